@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X-native HoverEnv step (the reference's hot path), env-steps/s.
+
+Workload (BASELINE.json metric): 65,536 HoverEnv envs per GPU, one process per GPU, global env
+ids contiguous per rank (a shard is bit-identical to the same ids on one GPU). One bench "step"
+= one fused quad_step launch over the rank's batch: CTBR-off HoverEnv.step (mixer, voltage sag,
+MuJoCo-equivalent physics, obs, reward, termination, truncation) + SB3 auto-reset, actions
+U[-1,1)^4 pre-generated in HBM (action_space.sample(), debug_training.py:111 / configs[1]).
+The timed loop replays hipGraphs of the step launches (launch-bound at this size).
+
+Prints ONE JSON line (rank 0). Also measured in the same run and reported as extra keys:
+per-launch kernel time from HIP event pairs (-> roofline), the 1M-env HBM-bound point, and the
+CPU baseline (the float64 oracle, 1 core, bounded sample) -- see DESIGN.md "Measurement".
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "env-steps/sec (whole node) at 65 536 hover envs, 1/2/4/8 MI355X"
+ENVS_PER_GPU = 65536
+BYTES_PER_ENV_STEP = 278  # state r/w 2x104, action 16, obs+rew+term+trunc 54
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def _quad_step_fn(env):
+    """Pre-built direct C-ABI call (no Python-side tensor ops per step)."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    L = N.lib()
+    out = N.QuadStepOut(obs=env.obs.data_ptr(), reward=env.reward.data_ptr(),
+                        terminated=env.terminated.data_ptr(), truncated=env.truncated.data_ptr(),
+                        terminal_obs=env.terminal_obs.data_ptr())
+    h = env._h
+
+    def step(actions_ptr: int):
+        s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        rc = L.quad_step(h, C.c_void_p(actions_ptr), C.byref(out), s)
+        if rc != 0:
+            N.check(rc, "quad_step")
+    return step
+
+
+def _kernel_time_us(env, step, actions, n_launch: int) -> float:
+    """Average device duration of one quad_step launch: HIP event pair around each launch on
+    the stream the kernel runs on (torch's current stream)."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(n_launch)]
+    torch.cuda.synchronize()
+    for k in range(n_launch):
+        ev[k][0].record()
+        step(actions[k % len(actions)].data_ptr())
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
+    return sum(ts[: max(1, int(0.9 * len(ts)))]) / max(1, int(0.9 * len(ts)))  # drop top 10 %
+
+
+def _run_rank(args, rank, world, local_rank):
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    n = args.envs
+    env = QuadVecEnv(n, env="hover", device=dev, seed=args.seed, env_id_base=rank * n)
+    env.reset()
+    n_act = min(args.action_batches, args.steps + args.warmup)
+    actions = [env.random_actions(k) for k in range(n_act)]  # resident in HBM
+    step = _quad_step_fn(env)
+    chunk = args.graph_chunk if args.steps % args.graph_chunk == 0 else args.steps
+
+    # warmup (eager), then capture the step sequence into a hipGraph
+    for k in range(args.warmup):
+        step(actions[k % n_act].data_ptr())
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for k in range(chunk):
+            step(actions[(args.warmup + k) % n_act].data_ptr())
+    torch.cuda.synchronize()
+
+    # timed region: exactly K steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps // chunk):
+        g.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-launch kernel time (roofline) on the same kernel, stream and data
+    k_us = _kernel_time_us(env, step, actions, args.kernel_launches)
+    res = dict(elapsed=elapsed, kernel_us=k_us)
+    if rank == 0 and args.large_envs > 0:
+        del actions, g
+        env.close()
+        torch.cuda.empty_cache()
+        big = QuadVecEnv(args.large_envs, env="hover", device=dev, seed=args.seed)
+        big.reset()
+        acts = [big.random_actions(k) for k in range(4)]
+        st = _quad_step_fn(big)
+        for k in range(5):
+            st(acts[k % 4].data_ptr())
+        res["large_kernel_us"] = _kernel_time_us(big, st, acts, 40)
+        big.close()
+    else:
+        env.close()
+    return res
+
+
+def _cpu_baseline(seconds: float) -> dict:
+    """The float64 CPU oracle (C restatement of HoverEnv + MuJoCo's step), one core, SB3
+    DummyVecEnv order (envs stepped one after another), random actions + auto-reset."""
+    from oracle import oracle as O
+    n_envs = 64
+    steps = 200
+    t0 = time.perf_counter()
+    O.bench_rollout(n_envs, steps, 0)
+    dt = time.perf_counter() - t0
+    steps = max(200, int(steps * seconds / max(dt, 1e-6)))
+    t0 = time.perf_counter()
+    O.bench_rollout(n_envs, steps, 0)
+    dt = time.perf_counter() - t0
+    return {"value": n_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/ float64 C restatement (HoverEnv + MuJoCo-equivalent mj_step + SB3 "
+                      f"auto-reset), {n_envs} envs x {steps} steps sequential, random actions, "
+                      f"1 thread, {dt:.1f} s on {platform.processor() or platform.machine()}"}
+
+
+def _pmc_traffic(n_envs: int):
+    """HBM bytes per quad_step launch from the committed rocprofv3 PMC summary, if present."""
+    path = os.path.join(REPO, "profiles", "pmc_quad_step.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d.get(str(n_envs), {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--envs", type=int, default=ENVS_PER_GPU)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--graph-chunk", type=int, default=100)
+    ap.add_argument("--action-batches", type=int, default=256)
+    ap.add_argument("--kernel-launches", type=int, default=200)
+    ap.add_argument("--large-envs", type=int, default=1 << 20)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    res = _run_rank(args, rank, world, local_rank)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank != 0:
+        return
+    n_total = args.envs * world
+    value = n_total * args.steps / res["elapsed"]
+    kus = res["kernel_us"]
+    achieved = BYTES_PER_ENV_STEP * args.envs / (kus * 1e-6) / 1e9
+    traffic = _pmc_traffic(args.envs)
+    line = {
+        "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": res["elapsed"] / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "HoverEnv step + SB3 auto-reset, random actions pre-generated in "
+                               "HBM (configs[1] step-kernel-only shape at the metric's 65,536 "
+                               "envs/GPU), hipGraph replay",
+                   "envs_per_gpu": args.envs, "global_envs": n_total,
+                   "parallelism": f"env-shard x{world} (no data-path collective)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "k_step<HOVER,noCTBR>", "kernel_us": kus,
+                     "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs},
+    }
+    if "large_kernel_us" in res:
+        lk = res["large_kernel_us"]
+        line["large_batch"] = {"envs": args.large_envs, "kernel_us": lk,
+                               "env_steps_per_s_kernel": args.large_envs / (lk * 1e-6),
+                               "achieved_GBs": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9}
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = _cpu_baseline(args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+/*
+ * quadenv.h -- C ABI of libquadenv.so, the MI355X-native vectorized quadrotor env.
+ *
+ * This is the drop-in boundary for the reference's hot path: N independent copies of
+ *   HoverEnv.step / HoverEnv.reset                 (envs/hover_env.py:159-198, :200-238)
+ *   RateControlWrapper.action / .step / .reset      (envs/rate_wrapper.py:69-111)
+ *   TrajectoryFollowEnv.step / .reset               (envs/trajectory_follow_env.py:145-174,
+ *                                                    :220-253)
+ * including the mujoco.mj_step they call (hover_env.py:180) and the SB3 VecEnv auto-reset
+ * around them (train.py:48, DummyVecEnv semantics), executed as HIP kernels on gfx950 over a
+ * struct-of-arrays batch resident in HBM.
+ *
+ * Conventions
+ *  - Plain C types only; `void* stream` is a hipStream_t (e.g. torch.cuda.current_stream()
+ *    .cuda_stream); NULL = the legacy default stream. Every call that launches work enqueues it
+ *    on that stream and returns without synchronizing (graph-capturable), except get/set_state
+ *    with host pointers, which synchronize the stream.
+ *  - Device pointers are caller-owned (torch tensors' data_ptr()); the handle owns only the env
+ *    state. Row-major shapes are given as [rows, cols].
+ *  - Return 0 on success, a negative QUAD_E* code on error; the message is available from
+ *    quad_last_error() (thread-local). Nothing aborts or throws across the ABI.
+ *  - A handle is bound to one device and is not internally locked (one handle per process per
+ *    GPU; multi-GPU = one process per GPU with disjoint env_id_base ranges).
+ */
+#ifndef QUADENV_H
+#define QUADENV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QUADENV_ABI_VERSION 1
+
+enum { QUAD_OK = 0, QUAD_EINVAL = -1, QUAD_EHIP = -2, QUAD_ENOMEM = -3, QUAD_EMODEL = -4 };
+enum { QUAD_ENV_HOVER = 0, QUAD_ENV_TRAJ = 1 };
+enum { QUAD_WRAP_NONE = 0, QUAD_WRAP_CTBR = 1 };
+enum { QUAD_NQ = 11, QUAD_NV = 10, QUAD_OBS = 12, QUAD_ACT = 4 };
+
+/* Env configuration. quad_default_cfg() fills the reference's defaults:
+ *  HoverEnv.__init__ (hover_env.py:15-100), TrajectoryFollowEnv.__init__
+ *  (trajectory_follow_env.py:22-104), RateControlWrapper.__init__ (rate_wrapper.py:40-64) with
+ *  pid_gains.json:43-52, drone_config.py:9-22, drone.xml:4 (timestep, gravity, fluid). */
+typedef struct QuadCfg {
+  int32_t env_kind;          /* QUAD_ENV_HOVER | QUAD_ENV_TRAJ */
+  int32_t wrapper;           /* QUAD_WRAP_NONE | QUAD_WRAP_CTBR (RateControlWrapper) */
+  int32_t max_episode_steps; /* 512 hover / 2048 traj */
+  int32_t auto_reset;        /* 1: SB3 VecEnv semantics (reset on terminated|truncated) */
+  float obs_low[12], obs_high[12];       /* HoverEnv._obs_bounds   (normalization) */
+  float init_low[12], init_high[12];     /* HoverEnv._initial_state_bounds */
+  float target_low[3], target_high[3];   /* HoverEnv._target_pos_bounds (hover only) */
+  float term_low[12], term_high[12];     /* HoverEnv._state_bounds (termination) */
+  float act_low[4], act_high[4];         /* HoverEnv._action_bounds */
+  double max_motor_thrust, arm_length, yaw_coeff;
+  double nominal_voltage, min_voltage, vdrop_base, vdrop_load;
+  double rate_max_rad, rate_kd[3], rate_ki, rate_imax, inertia[3], max_torque;
+  double timestep, gravity[3], density, viscosity;
+} QuadCfg;
+
+/* Env state in field-major SoA: each array is [fields][N] (qpos [11][N], qvel [10][N], ...).
+ * qpos = MuJoCo qpos (x y z qw qx qy qz theta1..4), qvel = MuJoCo qvel (world v, body omega,
+ * prop rates); voltage = HoverEnv.voltage; target = target_state.position; rate_int =
+ * RateControlWrapper._rate_int_torque; step_count = HoverEnv._step_count; episode = the number of
+ * resets drawn so far (the reset RNG counter). NULL members are skipped by get/set. */
+typedef struct QuadStateSoA {
+  float* qpos;
+  float* qvel;
+  float* voltage;
+  float* target;
+  float* rate_int;
+  int32_t* step_count;
+  uint32_t* episode;
+} QuadStateSoA;
+
+/* Outputs of quad_step (device pointers). Required: obs, reward, terminated, truncated.
+ *  obs            [N,12] normalized observation (after auto-reset for envs that finished)
+ *  reward         [N]    exp(-|pos - target|^2)           (hover_env.py:138-141)
+ *  terminated     [N]    NaN / state-bounds termination   (hover_env.py:150-157)
+ *  truncated      [N]    step_count >= max_episode_steps  (hover_env.py:188)
+ * Optional (NULL to skip):
+ *  terminal_obs   [N,12] obs before auto-reset (SB3 info["terminal_observation"]); only rows of
+ *                        envs that finished this step are written
+ *  motor_commands [N,4]  info["motor_commands"] (N)
+ *  voltage_scale  [N]    info["voltage_scale"]
+ *  state12        [N,12] info["state"]: absolute 12-D QuadState before auto-reset */
+typedef struct QuadStepOut {
+  float* obs;
+  float* reward;
+  uint8_t* terminated;
+  uint8_t* truncated;
+  float* terminal_obs;
+  float* motor_commands;
+  float* voltage_scale;
+  float* state12;
+} QuadStepOut;
+
+typedef struct QuadHandle QuadHandle;
+
+int quad_abi_version(void);
+const char* quad_last_error(void);
+
+/* Fill `cfg` with the reference defaults for (env_kind, wrapper); auto_reset = 1. */
+int quad_default_cfg(int32_t env_kind, int32_t wrapper, QuadCfg* cfg);
+
+/* Allocate N envs on `device`. Global env ids are env_id_base .. env_id_base+N-1; the reset RNG
+ * is Philox4x32-10 keyed by `seed` with counter (global env id, episode, draw block), so a
+ * shard's trajectories do not depend on how many GPUs the envs are spread over.
+ * State starts zeroed; call quad_reset before stepping. */
+int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_id_base,
+                int32_t n_envs, QuadHandle** out);
+void quad_destroy(QuadHandle* h);
+int32_t quad_num_envs(const QuadHandle* h);
+
+/* Re-key the reset RNG (HoverEnv.reset(seed=...), hover_env.py:210 -> gymnasium seeding) and
+ * zero every env's episode counter (stream-ordered). */
+int quad_seed(QuadHandle* h, uint64_t seed, void* stream);
+
+/* HoverEnv.reset for every env (mask == NULL) or for envs with mask[i] != 0 (device [N] u8).
+ * Writes the reset observation rows to obs (device [N,12]) when obs != NULL. */
+int quad_reset(QuadHandle* h, const uint8_t* mask, float* obs, void* stream);
+
+/* One vectorized env step: actions is device [N,4] float32 in the policy's normalized space
+ * (the CTBR wrapper's rate space when wrapper == QUAD_WRAP_CTBR). Not clipped by the env. */
+int quad_step(QuadHandle* h, const float* actions, const QuadStepOut* out, void* stream);
+
+/* HoverEnv._get_obs for the current state (e.g. after quad_set_state). obs: device [N,12];
+ * state12 (device [N,12] or NULL): the absolute QuadState vector (HoverEnv._state.vec()). */
+int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream);
+
+/* action_space.sample() equivalent for synthetic rollouts: U[-1,1)^4 per env from
+ * Philox(seed, global env id, step_index). actions: device [N,4]. */
+int quad_random_actions(QuadHandle* h, uint32_t step_index, float* actions, void* stream);
+
+/* Copy the env state out of / into the handle. `on_host` != 0: the SoA arrays are host memory
+ * (the call synchronizes `stream`); otherwise device memory (async). */
+int quad_get_state(QuadHandle* h, const QuadStateSoA* dst, int32_t on_host, void* stream);
+int quad_set_state(QuadHandle* h, const QuadStateSoA* src, int32_t on_host, void* stream);
+
+/* PPO rollout support (row P of the scope table): generalized advantage estimation over a
+ * time-major rollout, SB3 RolloutBuffer.compute_returns_and_advantage semantics.
+ *  rewards, values, episode_starts: device [T,N] float32 (episode_starts 1.0 where the step
+ *  began a new episode); last_values [N]; dones [N] (1.0 if the env finished at the last step).
+ *  Writes advantages and returns (= advantages + values), device [T,N]. */
+int quad_gae(const float* rewards, const float* values, const float* episode_starts,
+             const float* last_values, const float* dones, int32_t T, int32_t N, float gamma,
+             float gae_lambda, float* advantages, float* returns, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QUADENV_H */

@@ -91,6 +91,8 @@ def lib():
         L.oracle_reset_draw.argtypes = [C.POINTER(OracleCfg), C.c_uint64, C.c_uint64, C.c_uint32,
                                         fp, fp]
         L.oracle_random_action.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, fp]
+        L.oracle_bench_rollout.argtypes = [C.POINTER(OracleCfg), C.c_int32, C.c_int32, C.c_uint64]
+        L.oracle_bench_rollout.restype = C.c_double
         for n in ("oracle_sizeof_env", "oracle_sizeof_stepout", "oracle_sizeof_cfg"):
             getattr(L, n).restype = C.c_size_t
         assert L.oracle_sizeof_env() == C.sizeof(OracleEnv)
@@ -173,6 +175,12 @@ def random_action(seed: int, gid: int, step: int):
     a = np.zeros(4, np.float32)
     lib().oracle_random_action(seed, gid, step, _fp(a))
     return a
+
+
+def bench_rollout(n_envs: int, n_steps: int, seed: int = 0, env_kind: int = ENV_HOVER,
+                  wrapper: int = WRAP_NONE) -> float:
+    cfg = default_cfg(env_kind, wrapper)
+    return lib().oracle_bench_rollout(C.byref(cfg), n_envs, n_steps, seed)
 
 
 class Env:

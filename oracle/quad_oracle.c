@@ -784,6 +784,31 @@ void oracle_random_action(uint64_t seed, uint64_t gid, uint32_t step, float a[4]
   for (int i = 0; i < 4; i++) a[i] = (float)(r[i] >> 8) * 0x1p-23f - 1.0f;
 }
 
+double oracle_bench_rollout(const OracleCfg* cfg, int32_t n_envs, int32_t n_steps, uint64_t seed) {
+  OracleEnv envs[64];
+  uint32_t ep[64];
+  if (n_envs > 64) n_envs = 64;
+  double sum = 0;
+  float obs[12], i12[12], t3[3], a[4];
+  for (int i = 0; i < n_envs; i++) {
+    oracle_reset_draw(cfg, seed, (uint64_t)i, 0, i12, t3);
+    oracle_env_reset(cfg, &envs[i], i12, t3, obs);
+    ep[i] = 1;
+  }
+  OracleStepOut out;
+  for (int t = 0; t < n_steps; t++)
+    for (int i = 0; i < n_envs; i++) {
+      oracle_random_action(seed, (uint64_t)i, (uint32_t)t, a);
+      oracle_env_step(cfg, &envs[i], a, &out);
+      sum += out.reward;
+      if (out.terminated || out.truncated) {
+        oracle_reset_draw(cfg, seed, (uint64_t)i, ep[i]++, i12, t3);
+        oracle_env_reset(cfg, &envs[i], i12, t3, obs);
+      }
+    }
+  return sum;
+}
+
 size_t oracle_sizeof_env(void) { return sizeof(OracleEnv); }
 size_t oracle_sizeof_stepout(void) { return sizeof(OracleStepOut); }
 size_t oracle_sizeof_cfg(void) { return sizeof(OracleCfg); }

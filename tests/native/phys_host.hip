@@ -1,0 +1,88 @@
+// TEST INFRASTRUCTURE ONLY: instantiates the product's quad_physics.h templates on the host
+// (T = double and T = float) so tests/test_physics_host.py can cross-check the structured
+// closed-form step against the generic float64 oracle without a GPU. Not part of the product.
+#include "../../uav_reinforcement_learning_control_amd/csrc/quad_physics.h"
+
+using namespace quadenv;
+
+namespace {
+template <typename T>
+struct HostEnv {
+  KConsts<T> k;
+};
+
+template <typename T>
+void load(EnvRegs<T>& e, const double* qpos, const double* qvel, double volt, const float* tgt,
+          int32_t step, const double* rint) {
+  for (int i = 0; i < 3; i++) { e.pos[i] = T(qpos[i]); e.v[i] = T(qvel[i]); e.w[i] = T(qvel[3 + i]);
+    e.target[i] = tgt[i]; e.rint[i] = T(rint[i]); }
+  for (int i = 0; i < 4; i++) { e.q[i] = T(qpos[3 + i]); e.th[i] = T(qpos[7 + i]); e.s[i] = T(qvel[6 + i]); }
+  e.volt = T(volt);
+  e.step = step;
+}
+template <typename T>
+void save(const EnvRegs<T>& e, double* qpos, double* qvel, double* volt, int32_t* step, double* rint) {
+  for (int i = 0; i < 3; i++) { qpos[i] = e.pos[i]; qvel[i] = e.v[i]; qvel[3 + i] = e.w[i]; rint[i] = e.rint[i]; }
+  for (int i = 0; i < 4; i++) { qpos[3 + i] = e.q[i]; qpos[7 + i] = e.th[i]; qvel[6 + i] = e.s[i]; }
+  *volt = e.volt;
+  *step = e.step;
+}
+
+template <typename T>
+int step_impl(const QuadCfg* cfg, double* qpos, double* qvel, double* volt, const float* tgt,
+              int32_t* step, double* rint, const float* act, float* obs, float* s12, float* rew,
+              int32_t* term, int32_t* trunc, float* motor, float* vs) {
+  PhysConstsD d;
+  const char* why = "";
+  if (!make_phys_consts(*cfg, d, &why)) return -4;
+  KConsts<T> k;
+  make_kconsts<T>(*cfg, d, k);
+  EnvRegs<T> e;
+  load(e, qpos, qvel, *volt, tgt, *step, rint);
+  StepRes r;
+  if (cfg->wrapper == QUAD_WRAP_CTBR) env_step<T, true>(k, e, act, r);
+  else env_step<T, false>(k, e, act, r);
+  save(e, qpos, qvel, volt, step, rint);
+  for (int i = 0; i < 12; i++) { obs[i] = r.obs[i]; s12[i] = r.state12[i]; }
+  for (int i = 0; i < 4; i++) motor[i] = r.motor[i];
+  *rew = r.reward; *term = r.term; *trunc = r.trunc; *vs = r.vscale;
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+int host_env_step_f64(const QuadCfg* cfg, double* qpos, double* qvel, double* volt, const float* tgt,
+                      int32_t* step, double* rint, const float* act, float* obs, float* s12, float* rew,
+                      int32_t* term, int32_t* trunc, float* motor, float* vs) {
+  return step_impl<double>(cfg, qpos, qvel, volt, tgt, step, rint, act, obs, s12, rew, term, trunc, motor, vs);
+}
+int host_env_step_f32(const QuadCfg* cfg, double* qpos, double* qvel, double* volt, const float* tgt,
+                      int32_t* step, double* rint, const float* act, float* obs, float* s12, float* rew,
+                      int32_t* term, int32_t* trunc, float* motor, float* vs) {
+  return step_impl<float>(cfg, qpos, qvel, volt, tgt, step, rint, act, obs, s12, rew, term, trunc, motor, vs);
+}
+// physics only: qacc-free step of qpos/qvel under ctrl, T = double
+int host_physics_step_f64(const QuadCfg* cfg, double* qpos, double* qvel, const double* ctrl) {
+  PhysConstsD d;
+  const char* why = "";
+  if (!make_phys_consts(*cfg, d, &why)) return -4;
+  KConsts<double> k;
+  make_kconsts<double>(*cfg, d, k);
+  EnvRegs<double> e;
+  const float tgt[3] = {0, 0, 0};
+  const double rint[3] = {0, 0, 0};
+  load(e, qpos, qvel, 0.0, tgt, 0, rint);
+  physics_step(k.ph, e, ctrl);  // ctrl is float64 like MjData.ctrl
+  double v; int32_t s; double ri[3];
+  save(e, qpos, qvel, &v, &s, ri);
+  return 0;
+}
+void host_reset_draw(const QuadCfg* cfg, uint64_t seed, uint64_t gid, uint32_t ep, float* init12, float* tgt) {
+  PhysConstsD d;
+  const char* why = "";
+  make_phys_consts(*cfg, d, &why);
+  KConsts<float> k;
+  make_kconsts<float>(*cfg, d, k);
+  reset_draw(k.init_lo, k.init_span, k.tgt_lo, k.tgt_span, seed, gid, ep, init12, tgt);
+}
+}

@@ -1,0 +1,84 @@
+"""CPU checks of the C-ABI boundary: libquadenv.so builds, loads, exports every symbol
+include/quadenv.h declares, and its struct layouts match the Python binding (no GPU calls)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+import torch
+
+from uav_reinforcement_learning_control_amd import _native as N
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "quadenv.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|int32_t|const char\*)\s+(quad_\w+)\(", src, re.M)))
+
+
+def test_library_loads_and_version():
+    L = N.lib()
+    assert L.quad_abi_version() == N.ABI_VERSION
+
+
+def test_every_declared_symbol_is_exported():
+    L = N.lib()
+    decl = _declared()
+    assert len(decl) >= 14
+    for name in decl:
+        assert hasattr(L, name), name
+    assert sorted(N.EXPORTS) == decl
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True).stdout
+    for name in decl:
+        assert re.search(rf"\bT {name}\b", out), name
+
+
+def test_struct_layout_matches_header(tmp_path):
+    prog = tmp_path / "layout.c"
+    prog.write_text(f'''#include <stdio.h>
+#include <stddef.h>
+#include "{HEADER}"
+int main(void) {{
+  printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(QuadCfg), offsetof(QuadCfg, max_motor_thrust),
+         offsetof(QuadCfg, viscosity), sizeof(QuadStepOut), offsetof(QuadStepOut, state12),
+         sizeof(QuadStateSoA));
+  return 0;
+}}''')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(prog)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    want = [C.sizeof(N.QuadCfg), N.QuadCfg.max_motor_thrust.offset, N.QuadCfg.viscosity.offset,
+            C.sizeof(N.QuadStepOut), N.QuadStepOut.state12.offset, C.sizeof(N.QuadStateSoA)]
+    assert got == want
+
+
+def test_default_cfg_matches_reference_constants():
+    c = N.default_cfg(N.ENV_HOVER, N.WRAP_NONE)
+    assert c.max_episode_steps == 512 and c.auto_reset == 1
+    assert list(c.term_low[:3]) == [-2, -2, 0] and list(c.term_high[:3]) == [2, 2, 2]
+    assert abs(c.obs_high[3] - 3.1415927) < 1e-6 and c.act_high[0] == 52.0
+    assert c.nominal_voltage == 8.4 and c.min_voltage == 7.6
+    t = N.default_cfg(N.ENV_TRAJ, N.WRAP_CTBR)
+    assert t.max_episode_steps == 2048 and t.nominal_voltage == 16.8 and t.term_high[2] == 3
+    assert list(t.rate_kd) == [26, 26, 18] and t.rate_ki == 0.025 and t.rate_imax == 0.01
+    assert N.lib().quad_default_cfg(7, 0, C.byref(N.QuadCfg())) == N.QUAD_EINVAL
+    assert b"env_kind" in N.lib().quad_last_error()
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU error path")
+def test_create_without_gpu_fails_cleanly():
+    cfg = N.default_cfg()
+    h = C.c_void_p()
+    rc = N.lib().quad_create(C.byref(cfg), 0, 0, 0, 16, C.byref(h))
+    assert rc != 0 and not h.value
+    assert len(N.lib().quad_last_error()) > 0
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU error path")
+def test_env_refuses_to_run_without_gpu():
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    with pytest.raises(N.QuadError):
+        QuadVecEnv(8)

@@ -1,0 +1,113 @@
+"""ctypes binding of libquadenv.so (the C ABI in include/quadenv.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``csrc/Makefile`` -> ``_lib/``).
+There is no fallback: if the library is missing or fails to load, every env constructor raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "_lib", "libquadenv.so")
+CSRC = os.path.join(_PKG, "csrc")
+
+QUAD_OK, QUAD_EINVAL, QUAD_EHIP, QUAD_ENOMEM, QUAD_EMODEL = 0, -1, -2, -3, -4
+ENV_HOVER, ENV_TRAJ = 0, 1
+WRAP_NONE, WRAP_CTBR = 0, 1
+ABI_VERSION = 1
+
+
+class QuadCfg(C.Structure):
+    _fields_ = [
+        ("env_kind", C.c_int32), ("wrapper", C.c_int32), ("max_episode_steps", C.c_int32),
+        ("auto_reset", C.c_int32),
+        ("obs_low", C.c_float * 12), ("obs_high", C.c_float * 12),
+        ("init_low", C.c_float * 12), ("init_high", C.c_float * 12),
+        ("target_low", C.c_float * 3), ("target_high", C.c_float * 3),
+        ("term_low", C.c_float * 12), ("term_high", C.c_float * 12),
+        ("act_low", C.c_float * 4), ("act_high", C.c_float * 4),
+        ("max_motor_thrust", C.c_double), ("arm_length", C.c_double), ("yaw_coeff", C.c_double),
+        ("nominal_voltage", C.c_double), ("min_voltage", C.c_double),
+        ("vdrop_base", C.c_double), ("vdrop_load", C.c_double),
+        ("rate_max_rad", C.c_double), ("rate_kd", C.c_double * 3), ("rate_ki", C.c_double),
+        ("rate_imax", C.c_double), ("inertia", C.c_double * 3), ("max_torque", C.c_double),
+        ("timestep", C.c_double), ("gravity", C.c_double * 3), ("density", C.c_double),
+        ("viscosity", C.c_double),
+    ]
+
+
+class QuadStateSoA(C.Structure):
+    _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("voltage", C.c_void_p),
+                ("target", C.c_void_p), ("rate_int", C.c_void_p), ("step_count", C.c_void_p),
+                ("episode", C.c_void_p)]
+
+
+class QuadStepOut(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("reward", C.c_void_p), ("terminated", C.c_void_p),
+                ("truncated", C.c_void_p), ("terminal_obs", C.c_void_p),
+                ("motor_commands", C.c_void_p), ("voltage_scale", C.c_void_p),
+                ("state12", C.c_void_p)]
+
+
+# every symbol include/quadenv.h declares (checked by tests/test_abi.py)
+EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_create",
+           "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_observe",
+           "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae")
+
+
+class QuadError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def _declare(L):
+    vp, i32, u32, u64 = C.c_void_p, C.c_int32, C.c_uint32, C.c_uint64
+    L.quad_abi_version.restype = C.c_int
+    L.quad_last_error.restype = C.c_char_p
+    L.quad_default_cfg.argtypes = [i32, i32, C.POINTER(QuadCfg)]
+    L.quad_create.argtypes = [C.POINTER(QuadCfg), i32, u64, u64, i32, C.POINTER(vp)]
+    L.quad_destroy.argtypes = [vp]
+    L.quad_destroy.restype = None
+    L.quad_num_envs.argtypes = [vp]
+    L.quad_num_envs.restype = i32
+    L.quad_seed.argtypes = [vp, u64, vp]
+    L.quad_reset.argtypes = [vp, vp, vp, vp]
+    L.quad_step.argtypes = [vp, vp, C.POINTER(QuadStepOut), vp]
+    L.quad_observe.argtypes = [vp, vp, vp, vp]
+    L.quad_random_actions.argtypes = [vp, u32, vp, vp]
+    L.quad_get_state.argtypes = [vp, C.POINTER(QuadStateSoA), i32, vp]
+    L.quad_set_state.argtypes = [vp, C.POINTER(QuadStateSoA), i32, vp]
+    L.quad_gae.argtypes = [vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
+    for n in ("quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_observe",
+              "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae"):
+        getattr(L, n).restype = C.c_int
+
+
+def lib():
+    """Load libquadenv.so; raise loudly if it is absent (no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise QuadError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; "
+                            f"g.build()'` (or make -C {CSRC}) to build the HIP extension")
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        if L.quad_abi_version() != ABI_VERSION:
+            raise QuadError("libquadenv.so ABI version mismatch; rebuild it")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != QUAD_OK:
+        msg = lib().quad_last_error().decode(errors="replace")
+        raise QuadError(f"{what} failed ({rc}): {msg}")
+
+
+def default_cfg(env_kind: int = ENV_HOVER, wrapper: int = WRAP_NONE) -> QuadCfg:
+    cfg = QuadCfg()
+    check(lib().quad_default_cfg(env_kind, wrapper, C.byref(cfg)), "quad_default_cfg")
+    return cfg

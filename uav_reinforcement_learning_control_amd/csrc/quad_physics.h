@@ -1,0 +1,582 @@
+// quad_physics.h -- one env step of the reference hot path, as __host__ __device__ templates.
+//
+// T = float is what the gfx950 kernels run (state resident in HBM as float32 SoA). The same
+// source instantiated with T = double on the host is cross-checked against the independent
+// generic float64 oracle (oracle/quad_oracle.c) to 1e-12 in tests/test_physics_host.py, which
+// is how the structured closed form below is verified without a GPU.
+//
+// Reference semantics reproduced (file:line into the reference):
+//   RateControlWrapper.action            envs/rate_wrapper.py:69-98
+//   denormalize (float32)                utils/normalization.py:20-30   (hover_env.py:169)
+//   _mix_to_motors, voltage sag          envs/hover_env.py:102-124, 173-176
+//   mujoco.mj_step                       envs/hover_env.py:180 (MuJoCo 3.x Euler step; see below)
+//   QuadState.set_from_mujoco (scipy)    utils/state.py:28-46
+//   _get_obs + normalize (float32)       envs/hover_env.py:126-136, utils/normalization.py:7-17
+//   _get_reward                          envs/hover_env.py:138-141
+//   _is_terminated, truncation           envs/hover_env.py:150-157, 182-188
+//   reset / random_reset / set_state     envs/hover_env.py:200-238, utils/state.py:48-65,90-98
+//   TrajectoryFollowEnv differences      envs/trajectory_follow_env.py:24-26,60-63,220-253
+//
+// The physics is MuJoCo's Euler step for drone.xml in closed form (quad_model.h explains the
+// reduction): generalized speeds u = (v_world, w_body, s_1..4); forces from the motors (site
+// transmission), gravity and the inertia-box fluid model on all five bodies; bias from the exact
+// Newton-Euler velocity products; qacc from the 3x3 Schur-reduced solve; then semi-implicit Euler
+// with MuJoCo's quaternion integration. MuJoCo's mj_checkPos/Vel/Acc resets and its bad-ctrl
+// zeroing are reproduced.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "quad_model.h"
+
+#define QD_HD __host__ __device__ __forceinline__
+
+namespace quadenv {
+
+// ---------------------------------------------------------------------------------------------
+// math shims resolving to the right precision (no dual code paths: both are plain HIP)
+QD_HD float q_sqrt(float x) { return sqrtf(x); }
+QD_HD double q_sqrt(double x) { return sqrt(x); }
+QD_HD float q_atan2(float y, float x) { return atan2f(y, x); }
+QD_HD double q_atan2(double y, double x) { return atan2(y, x); }
+QD_HD float q_hypot(float x, float y) { return hypotf(x, y); }
+QD_HD double q_hypot(double x, double y) { return hypot(x, y); }
+QD_HD float q_abs(float x) { return fabsf(x); }
+QD_HD double q_abs(double x) { return fabs(x); }
+QD_HD float q_exp(float x) { return expf(x); }
+QD_HD double q_exp(double x) { return exp(x); }
+QD_HD void q_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+QD_HD void q_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+
+// np.clip semantics: NaN propagates
+template <typename T>
+QD_HD T clipn(T x, T lo, T hi) {
+  return (x != x) ? x : (x < lo ? lo : (x > hi ? hi : x));
+}
+// mju_isBad
+template <typename T>
+QD_HD bool isbad(T x) {
+  return !(x == x) || x > T(1e10) || x < T(-1e10);
+}
+
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+struct PhysConsts {
+  T mt, inv_mt, cbar[3], IO[9], Ainv[9], c_ax, inv_c_ax;
+  T pc[4][3], sx[4], sy[4], g5[4];
+  T b_kql[3], b_kqa[3], b_kvl, b_kva;
+  T p_kql[3], p_kqa[3], p_kvl, p_kva;
+  T gz, dt;
+  // control path (mixer, voltage, motor wrench) stays float64: four ~13 N motor forces cancel
+  // to mN*m torques, which float32 cannot resolve to the 1e-5 parity bar
+  double sxd[4], syd[4], g5d[4], ctrl_lo, ctrl_hi;
+  double mix[16];
+};
+
+template <typename T>
+struct KConsts {
+  PhysConsts<T> ph;
+  // float32 env constants (the reference keeps these as float32 Box bounds)
+  float obs_lo[12], obs_span[12];   // span = high - low, computed in float32 like NumPy
+  float term_lo[12], term_hi[12];
+  float act_lo[4], act_span[4];
+  float init_lo[12], init_span[12];
+  float tgt_lo[3], tgt_span[3];
+  // float64 in the reference (Python floats / float64 arrays)
+  double max_thrust, vnom, vmin, vb, vl, dt;
+  double rate_max, rate_ikd[3], rate_kidt, rate_imax, max_torque;
+  int32_t max_steps;
+};
+
+template <typename T>
+inline void make_kconsts(const QuadCfg& cfg, const PhysConstsD& d, KConsts<T>& k) {
+  PhysConsts<T>& p = k.ph;
+  p.mt = T(d.mt); p.inv_mt = T(d.inv_mt); p.c_ax = T(d.c_ax); p.inv_c_ax = T(d.inv_c_ax);
+  for (int i = 0; i < 3; i++) {
+    p.cbar[i] = T(d.cbar[i]);
+    p.b_kql[i] = T(d.b_kql[i]); p.b_kqa[i] = T(d.b_kqa[i]);
+    p.p_kql[i] = T(d.p_kql[i]); p.p_kqa[i] = T(d.p_kqa[i]);
+  }
+  for (int i = 0; i < 9; i++) { p.IO[i] = T(d.IO[i]); p.Ainv[i] = T(d.Ainv[i]); }
+  for (int i = 0; i < 4; i++) {
+    for (int j = 0; j < 3; j++) p.pc[i][j] = T(d.pc[i][j]);
+    p.sx[i] = T(d.sx[i]); p.sy[i] = T(d.sy[i]); p.g5[i] = T(d.g5[i]);
+    p.sxd[i] = d.sx[i]; p.syd[i] = d.sy[i]; p.g5d[i] = d.g5[i];
+  }
+  for (int i = 0; i < 16; i++) p.mix[i] = d.mix[i];
+  p.b_kvl = T(d.b_kvl); p.b_kva = T(d.b_kva); p.p_kvl = T(d.p_kvl); p.p_kva = T(d.p_kva);
+  p.gz = T(d.gz); p.dt = T(d.dt); p.ctrl_lo = d.ctrl_lo; p.ctrl_hi = d.ctrl_hi;
+  for (int i = 0; i < 12; i++) {
+    k.obs_lo[i] = cfg.obs_low[i];
+    k.obs_span[i] = cfg.obs_high[i] - cfg.obs_low[i];
+    k.term_lo[i] = cfg.term_low[i];
+    k.term_hi[i] = cfg.term_high[i];
+    k.init_lo[i] = cfg.init_low[i];
+    k.init_span[i] = cfg.init_high[i] - cfg.init_low[i];
+  }
+  for (int i = 0; i < 4; i++) {
+    k.act_lo[i] = cfg.act_low[i];
+    k.act_span[i] = cfg.act_high[i] - cfg.act_low[i];
+  }
+  for (int i = 0; i < 3; i++) {
+    k.tgt_lo[i] = cfg.target_low[i];
+    k.tgt_span[i] = cfg.target_high[i] - cfg.target_low[i];
+  }
+  k.max_thrust = cfg.max_motor_thrust;
+  k.vnom = cfg.nominal_voltage; k.vmin = cfg.min_voltage;
+  k.vb = cfg.vdrop_base; k.vl = cfg.vdrop_load; k.dt = cfg.timestep;
+  k.rate_max = cfg.rate_max_rad;
+  for (int i = 0; i < 3; i++) k.rate_ikd[i] = cfg.inertia[i] * cfg.rate_kd[i];
+  k.rate_kidt = cfg.rate_ki * cfg.timestep;
+  k.rate_imax = cfg.rate_imax;
+  k.max_torque = cfg.max_torque;
+  k.max_steps = cfg.max_episode_steps;
+}
+
+// Per-env state held in registers for one step.
+template <typename T>
+struct EnvRegs {
+  T pos[3], q[4], th[4];  // qpos
+  T v[3], w[3], s[4];     // qvel
+  T volt;
+  T rint[3];
+  float target[3];
+  int32_t step;
+};
+
+struct StepRes {
+  float obs[12];
+  float state12[12];
+  float reward;
+  float motor[4];
+  float vscale;
+  bool term, trunc;
+};
+
+// ---------------------------------------------------------------------------------------------
+// physics
+template <typename T>
+QD_HD void cross(const T a[3], const T b[3], T r[3]) {
+  r[0] = a[1] * b[2] - a[2] * b[1];
+  r[1] = a[2] * b[0] - a[0] * b[2];
+  r[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// mj_inertiaBoxFluidModel in the body's own axes: t = -kv_a w - kq_a |w| w, f likewise
+template <typename T>
+QD_HD void box_drag(const T w[3], const T u[3], const T kqa[3], const T kva, const T kql[3],
+                    const T kvl, T t[3], T f[3]) {
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    t[j] = -kva * w[j] - kqa[j] * q_abs(w[j]) * w[j];
+    f[j] = -kvl * u[j] - kql[j] * q_abs(u[j]) * u[j];
+  }
+}
+
+// qacc of the free base + 4 props at (q, v, w, s, th) under the motor wrench (total thrust
+// along base z and torque about the base origin, base frame). Outputs: vdot (world),
+// wdot (body), sdot[4].
+template <typename T>
+QD_HD void forward_acc(const PhysConsts<T>& c, const T qn[4], const T th[4], const T v[3],
+                       const T w[3], const T s[4], const T Fsum, const T taum[3], T vdot[3],
+                       T wdot[3], T sdot[4]) {
+  // R = quat2mat(q) (q already normalized)
+  const T qw = qn[0], qx = qn[1], qy = qn[2], qz = qn[3];
+  T R[9];
+  R[0] = T(1) - T(2) * (qy * qy + qz * qz); R[1] = T(2) * (qx * qy - qw * qz); R[2] = T(2) * (qx * qz + qw * qy);
+  R[3] = T(2) * (qx * qy + qw * qz); R[4] = T(1) - T(2) * (qx * qx + qz * qz); R[5] = T(2) * (qy * qz - qw * qx);
+  R[6] = T(2) * (qx * qz - qw * qy); R[7] = T(2) * (qy * qz + qw * qx); R[8] = T(1) - T(2) * (qx * qx + qy * qy);
+  T vB[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) vB[i] = R[i] * v[0] + R[3 + i] * v[1] + R[6 + i] * v[2];
+
+  // total external force (base frame) and torque about the base origin (base frame)
+  T FB[3] = {T(0), T(0), Fsum};
+  T tau[3] = {taum[0], taum[1], taum[2]};
+  // gravity on every body COM: M g at cbar
+  {
+    const T mg = c.mt * c.gz;
+    const T gB[3] = {mg * R[6], mg * R[7], mg * R[8]};
+    T t[3];
+    cross(c.cbar, gB, t);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { FB[i] += gB[i]; tau[i] += t[i]; }
+  }
+  // base fluid: body frame == principal frame, COM at the origin
+  {
+    T t[3], f[3];
+    box_drag(w, vB, c.b_kqa, c.b_kva, c.b_kql, c.b_kvl, t, f);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { FB[i] += f[i]; tau[i] += t[i]; }
+  }
+  // prop fluid: prop frame = base frame rotated by th_i about z; COM on the axis at pc_i
+  T Qs[4];
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    T sn, cs;
+    q_sincos(th[p], &sn, &cs);
+    T wxc[3];
+    cross(w, c.pc[p], wxc);
+    const T ub[3] = {vB[0] + wxc[0], vB[1] + wxc[1], vB[2] + wxc[2]};
+    const T wp[3] = {cs * w[0] + sn * w[1], -sn * w[0] + cs * w[1], w[2] + s[p]};
+    const T up[3] = {cs * ub[0] + sn * ub[1], -sn * ub[0] + cs * ub[1], ub[2]};
+    T tp[3], fp[3];
+    box_drag(wp, up, c.p_kqa, c.p_kva, c.p_kql, c.p_kvl, tp, fp);
+    const T f[3] = {cs * fp[0] - sn * fp[1], sn * fp[0] + cs * fp[1], fp[2]};
+    const T t[3] = {cs * tp[0] - sn * tp[1], sn * tp[0] + cs * tp[1], tp[2]};
+    T rxf[3];
+    cross(c.pc[p], f, rxf);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { FB[i] += f[i]; tau[i] += rxf[i] + t[i]; }
+    Qs[p] = tp[2];
+  }
+  // velocity-product (bias) terms
+  T wc[3], wwc[3];
+  cross(w, c.cbar, wc);
+  cross(w, wc, wwc);
+  T fv[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) fv[i] = FB[i] - c.mt * wwc[i];
+  T Iw[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) Iw[i] = c.IO[3 * i] * w[0] + c.IO[3 * i + 1] * w[1] + c.IO[3 * i + 2] * w[2];
+  T wIw[3];
+  cross(w, Iw, wIw);
+  const T ssum = s[0] + s[1] + s[2] + s[3];
+  const T Qsum = Qs[0] + Qs[1] + Qs[2] + Qs[3];
+  T cxf[3];
+  cross(c.cbar, fv, cxf);
+  T rhs[3];
+  rhs[0] = tau[0] - wIw[0] - c.c_ax * ssum * w[1] - cxf[0];
+  rhs[1] = tau[1] - wIw[1] + c.c_ax * ssum * w[0] - cxf[1];
+  rhs[2] = tau[2] - wIw[2] - Qsum - cxf[2];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+    wdot[i] = c.Ainv[3 * i] * rhs[0] + c.Ainv[3 * i + 1] * rhs[1] + c.Ainv[3 * i + 2] * rhs[2];
+  T cxw[3];
+  cross(c.cbar, wdot, cxw);
+  T aB[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) aB[i] = fv[i] * c.inv_mt + cxw[i];
+#pragma unroll
+  for (int i = 0; i < 3; i++) vdot[i] = R[3 * i] * aB[0] + R[3 * i + 1] * aB[1] + R[3 * i + 2] * aB[2];
+#pragma unroll
+  for (int p = 0; p < 4; p++) sdot[p] = Qs[p] * c.inv_c_ax - wdot[2];
+}
+
+template <typename T>
+QD_HD void normalize4(T q[4]) {
+  const T n = q_sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < T(1e-15)) {
+    q[0] = T(1); q[1] = q[2] = q[3] = T(0);
+  } else {
+    const T inv = T(1) / n;
+    q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv;
+  }
+}
+
+// mujoco.mj_step for one env. Fin: ctrl in float64 (may be NaN / out of range; MuJoCo semantics).
+template <typename T>
+QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4]) {
+  // mj_checkPos / mj_checkVel: bad state => mj_resetData (qpos0, zero qvel, zero ctrl)
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < 3; i++) bad |= int(isbad(e.pos[i])) | int(isbad(e.v[i])) | int(isbad(e.w[i]));
+#pragma unroll
+  for (int i = 0; i < 4; i++) bad |= int(isbad(e.q[i])) | int(isbad(e.th[i])) | int(isbad(e.s[i]));
+  bool badctrl = false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) badctrl |= isbad(Fin[i]);
+  if (bad) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) { e.pos[i] = T(0); e.v[i] = T(0); e.w[i] = T(0); }
+    e.q[0] = T(1); e.q[1] = e.q[2] = e.q[3] = T(0);
+#pragma unroll
+    for (int i = 0; i < 4; i++) { e.th[i] = T(0); e.s[i] = T(0); }
+    badctrl = true;
+  }
+  // mj_fwdActuation: bad ctrl => all ctrl zeroed; ctrlrange clamp; site-transmission wrench
+  double F[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double f = badctrl ? 0.0 : Fin[i];
+    F[i] = f < c.ctrl_lo ? c.ctrl_lo : (f > c.ctrl_hi ? c.ctrl_hi : f);
+  }
+  T Fsum = T(F[0] + F[1] + F[2] + F[3]);
+  T taum[3] = {T(c.syd[0] * F[0] + c.syd[1] * F[1] + c.syd[2] * F[2] + c.syd[3] * F[3]),
+               T(-(c.sxd[0] * F[0] + c.sxd[1] * F[1] + c.sxd[2] * F[2] + c.sxd[3] * F[3])),
+               T(c.g5d[0] * F[0] + c.g5d[1] * F[1] + c.g5d[2] * F[2] + c.g5d[3] * F[3])};
+  T qn[4] = {e.q[0], e.q[1], e.q[2], e.q[3]};
+  normalize4(qn);
+  T vdot[3], wdot[3], sdot[4];
+  forward_acc(c, qn, e.th, e.v, e.w, e.s, Fsum, taum, vdot, wdot, sdot);
+  bool badacc = false;
+#pragma unroll
+  for (int i = 0; i < 3; i++) badacc |= int(isbad(vdot[i])) | int(isbad(wdot[i]));
+#pragma unroll
+  for (int i = 0; i < 4; i++) badacc |= isbad(sdot[i]);
+  if (badacc) {  // mj_checkAcc: reset, recompute at qpos0 with zero ctrl
+#pragma unroll
+    for (int i = 0; i < 3; i++) { e.pos[i] = T(0); e.v[i] = T(0); e.w[i] = T(0); taum[i] = T(0); }
+    e.q[0] = T(1); e.q[1] = e.q[2] = e.q[3] = T(0);
+#pragma unroll
+    for (int i = 0; i < 4; i++) { e.th[i] = T(0); e.s[i] = T(0); }
+    Fsum = T(0);
+    qn[0] = T(1); qn[1] = qn[2] = qn[3] = T(0);
+    forward_acc(c, qn, e.th, e.v, e.w, e.s, Fsum, taum, vdot, wdot, sdot);
+  }
+  // mj_Euler -> mj_advance: qvel += h qacc, then positions with the new qvel
+  const T h = c.dt;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    e.v[i] += h * vdot[i];
+    e.w[i] += h * wdot[i];
+    e.pos[i] += h * e.v[i];
+  }
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    e.s[p] += h * sdot[p];
+    e.th[p] += h * e.s[p];
+  }
+  // mju_quatIntegrate(quat, w, h): quat = normalize(quat) * axisangle(w/|w|, h |w|)
+  const T wn = q_sqrt(e.w[0] * e.w[0] + e.w[1] * e.w[1] + e.w[2] * e.w[2]);
+  T qr[4];
+  if (wn < T(1e-15)) {
+    qr[0] = T(1); qr[1] = qr[2] = qr[3] = T(0);
+  } else {
+    T sh, ch;
+    q_sincos(T(0.5) * h * wn, &sh, &ch);
+    const T k = sh / wn;
+    qr[0] = ch; qr[1] = e.w[0] * k; qr[2] = e.w[1] * k; qr[3] = e.w[2] * k;
+  }
+  const T a0 = qn[0], a1 = qn[1], a2 = qn[2], a3 = qn[3];
+  e.q[0] = a0 * qr[0] - a1 * qr[1] - a2 * qr[2] - a3 * qr[3];
+  e.q[1] = a0 * qr[1] + a1 * qr[0] + a2 * qr[3] - a3 * qr[2];
+  e.q[2] = a0 * qr[2] - a1 * qr[3] + a2 * qr[0] + a3 * qr[1];
+  e.q[3] = a0 * qr[3] + a1 * qr[2] - a2 * qr[1] + a3 * qr[0];
+}
+
+// ---------------------------------------------------------------------------------------------
+// scipy Rotation.from_quat(xyzw).as_euler('xyz') (utils/state.py:42): Bernardes & Viollet
+template <typename T>
+QD_HD void quat_to_euler(const T qin[4], T e[3]) {
+  T q[4] = {qin[0], qin[1], qin[2], qin[3]};
+  const T n = q_sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const T inv = T(1) / n;
+  const T qw = q[0] * inv, qx = q[1] * inv, qy = q[2] * inv, qz = q[3] * inv;
+  const T a = qw - qy, b = qx + qz, c = qy + qw, d = qz - qx;
+  const T PI = T(3.14159265358979323846);
+  T mid = T(2) * q_atan2(q_hypot(c, d), q_hypot(a, b));
+  const bool case1 = q_abs(mid) <= T(1e-7), case2 = q_abs(mid - PI) <= T(1e-7);
+  const T hs = q_atan2(b, a), hd = q_atan2(d, c);
+  if (!(case1 || case2)) {
+    e[0] = hs - hd;
+    e[2] = hs + hd;
+  } else {
+    e[2] = T(0);
+    e[0] = case1 ? T(2) * hs : T(-2) * hd;
+  }
+  e[1] = mid - PI / T(2);
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    if (e[i] < -PI) e[i] += T(2) * PI;
+    else if (e[i] > PI) e[i] -= T(2) * PI;
+  }
+}
+
+// scipy Rotation.from_euler('xyz', e).as_quat() (utils/state.py:59) -> wxyz
+template <typename T>
+QD_HD void euler_to_quat(const T e[3], T q[4]) {
+  T sr, cr, sp, cp, sy, cy;
+  q_sincos(e[0] * T(0.5), &sr, &cr);
+  q_sincos(e[1] * T(0.5), &sp, &cp);
+  q_sincos(e[2] * T(0.5), &sy, &cy);
+  q[0] = cy * cp * cr + sy * sp * sr;
+  q[1] = cy * cp * sr - sy * sp * cr;
+  q[2] = cy * sp * cr + sy * cp * sr;
+  q[3] = sy * cp * cr - cy * sp * sr;
+}
+
+// normalize (utils/normalization.py:7-17) in float32, no contraction, NumPy's operation order
+QD_HD float norm_obs1(float x, float lo, float span) {
+#pragma clang fp contract(off)
+  const float t = x - lo;
+  const float u = 2.0f * t;
+  const float v = u / span;
+  return v - 1.0f;
+}
+// denormalize (utils/normalization.py:20-30) in float32
+QD_HD float denorm1(float a, float lo, float span) {
+#pragma clang fp contract(off)
+  const float s = a + 1.0f;
+  const float h = s / 2.0f;
+  const float m = h * span;
+  return m + lo;
+}
+QD_HD float sub32(float a, float b) {
+#pragma clang fp contract(off)
+  return a - b;
+}
+
+template <typename T>
+QD_HD void observe(const KConsts<T>& k, const EnvRegs<T>& e, float obs[12], float s12[12]) {
+  T eul[3];
+  quat_to_euler(e.q, eul);
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    s12[i] = float(e.pos[i]);
+    s12[3 + i] = float(eul[i]);
+    s12[6 + i] = float(e.v[i]);
+    s12[9 + i] = float(e.w[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const float x = i < 3 ? sub32(e.target[i], s12[i]) : s12[i];
+    obs[i] = norm_obs1(x, k.obs_lo[i], k.obs_span[i]);
+  }
+}
+
+// reward = exp(-|pos - target|^2); the norm is NumPy's float32 sdot (products rounded to float32,
+// float64 accumulation) then float32 sqrt -- see oracle/quad_oracle.c.
+template <typename T>
+QD_HD float reward_of(const float s12[12], const float tgt[3]) {
+  double acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const float d = sub32(s12[i], tgt[i]);
+    float p;
+    {
+#pragma clang fp contract(off)
+      p = d * d;
+    }
+    acc += double(p);
+  }
+  const T pe = T(sqrtf(float(acc)));
+  return float(q_exp(-(pe * pe)));
+}
+
+template <typename T>
+QD_HD bool terminated_of(const KConsts<T>& k, const float s12[12]) {
+  bool t = false;
+#pragma unroll
+  for (int i = 0; i < 12; i++) t |= !(s12[i] >= k.term_lo[i] && s12[i] <= k.term_hi[i]);
+  return t;  // a NaN fails both compares; +-Inf is outside any finite bound
+}
+
+// (RateControlWrapper.action ->) HoverEnv.step for one env. The control path (CTBR, mixer,
+// voltage sag) runs in float64 like the reference; the rigid-body dynamics in T.
+template <typename T, bool CTBR>
+QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], StepRes& r) {
+  float a[4];
+  a[0] = act[0];
+  if (CTBR) {
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const double des = double(act[1 + j]) * k.rate_max;
+      const double err = des - double(float(e.w[j]));  // _state.angular_velocity is float32
+      const double taup = k.rate_ikd[j] * err;
+      const double ri = clipn(double(e.rint[j]) + k.rate_kidt * err, -k.rate_imax, k.rate_imax);
+      e.rint[j] = T(ri);
+      const double tau = taup + ri;
+      a[1 + j] = float(clipn(tau / k.max_torque, -1.0, 1.0));
+    }
+  } else {
+    a[1] = act[1]; a[2] = act[2]; a[3] = act[3];
+  }
+  double phys[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) phys[j] = double(denorm1(a[j], k.act_lo[j], k.act_span[j]));
+  double F[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double s = k.ph.mix[4 * i] * phys[0] + k.ph.mix[4 * i + 1] * phys[1] +
+                     k.ph.mix[4 * i + 2] * phys[2] + k.ph.mix[4 * i + 3] * phys[3];
+    F[i] = clipn(s, 0.0, k.max_thrust);
+  }
+  const double vs = clipn(double(e.volt) / k.vnom, 0.0, 1.0);
+#pragma unroll
+  for (int i = 0; i < 4; i++) F[i] = clipn(F[i] * vs, 0.0, k.max_thrust * vs);
+  const double mx = k.max_thrust > 1e-6 ? k.max_thrust : 1e-6;
+  const double load = ((F[0] + F[1] + F[2] + F[3]) / 4.0) / mx;
+  const double dV = (k.vb + k.vl * load) * k.dt;
+  e.volt = T(clipn(double(e.volt) - dV, k.vmin, k.vnom));
+  physics_step(k.ph, e, F);
+  e.step += 1;
+  observe(k, e, r.obs, r.state12);
+  r.reward = reward_of<T>(r.state12, e.target);
+  r.term = terminated_of(k, r.state12);
+  r.trunc = e.step >= k.max_steps;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r.motor[i] = float(F[i]);
+  r.vscale = float(vs);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al. 2011) and the reset / action draws
+QD_HD void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t p0 = uint64_t(0xD2511F53u) * c[0];
+    const uint64_t p1 = uint64_t(0xCD9E8D57u) * c[2];
+    const uint32_t n0 = uint32_t(p1 >> 32) ^ c[1] ^ k0;
+    const uint32_t n2 = uint32_t(p0 >> 32) ^ c[3] ^ k1;
+    c[0] = n0; c[1] = uint32_t(p1); c[2] = n2; c[3] = uint32_t(p0);
+  }
+}
+QD_HD float u01(uint32_t x) { return float(x >> 8) * 0x1p-24f; }
+QD_HD float affine32(float lo, float u, float span) {
+#pragma clang fp contract(off)
+  const float m = u * span;
+  return lo + m;
+}
+
+// Draws for HoverEnv.reset: 12 init-state values then 3 target values (QuadState.random_reset +
+// the target draw, hover_env.py:219-228), Philox-keyed by (seed; global env id, episode, block).
+QD_HD void reset_draw(const float init_lo[12], const float init_span[12], const float tgt_lo[3],
+                      const float tgt_span[3], uint64_t seed, uint64_t gid, uint32_t episode,
+                      float init12[12], float tgt[3]) {
+  uint32_t r[16];
+#pragma unroll
+  for (uint32_t blk = 0; blk < 4; blk++) {
+    uint32_t c[4] = {uint32_t(gid), uint32_t(gid >> 32), episode, blk};
+    philox4x32_10(c, uint32_t(seed), uint32_t(seed >> 32));
+    r[4 * blk] = c[0]; r[4 * blk + 1] = c[1]; r[4 * blk + 2] = c[2]; r[4 * blk + 3] = c[3];
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) init12[i] = affine32(init_lo[i], u01(r[i]), init_span[i]);
+#pragma unroll
+  for (int i = 0; i < 3; i++) tgt[i] = affine32(tgt_lo[i], u01(r[12 + i]), tgt_span[i]);
+}
+
+// HoverEnv.reset / TrajectoryFollowEnv.reset given the draws; writes the reset obs.
+template <typename T, int KIND>
+QD_HD void env_reset_from(const KConsts<T>& k, EnvRegs<T>& e, const float init12[12],
+                          const float tgt[3], float obs[12], float s12[12]) {
+  T eul[3] = {T(init12[3]), T(init12[4]), T(init12[5])};
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    e.pos[i] = T(init12[i]);
+    e.v[i] = T(init12[6 + i]);
+    e.w[i] = T(init12[9 + i]);
+    e.rint[i] = T(0);
+    // TrajectoryFollowEnv: target = traj_pos[0] = start position (trajectory_follow_env.py:242-243)
+    e.target[i] = KIND == QUAD_ENV_TRAJ ? init12[i] : tgt[i];
+  }
+  euler_to_quat(eul, e.q);
+#pragma unroll
+  for (int p = 0; p < 4; p++) { e.th[p] = T(0); e.s[p] = T(0); }
+  e.volt = T(k.vnom);
+  e.step = 0;
+  // QuadState.set_from_mujoco(get_mujoco_state()) returns the drawn attitude: use it directly
+#pragma unroll
+  for (int i = 0; i < 12; i++) s12[i] = init12[i];
+#pragma unroll
+  for (int i = 0; i < 12; i++) {
+    const float x = i < 3 ? sub32(e.target[i], s12[i]) : s12[i];
+    obs[i] = norm_obs1(x, k.obs_lo[i], k.obs_span[i]);
+  }
+}
+
+}  // namespace quadenv
