@@ -89,25 +89,31 @@ def _run_rank(args, rank, world, local_rank):
             step(actions[(args.warmup + k) % n_act].data_ptr())
     torch.cuda.synchronize()
 
-    # timed region: exactly K steps
+    # timed region: exactly K steps; HIP events on the stream the kernels run on give the
+    # average launch duration (graph replay leaves no host gap between launches)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record()
     for _ in range(args.steps // chunk):
         g.replay()
+    e1.record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    launch_us = e0.elapsed_time(e1) * 1e3 / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     # per-launch kernel time (roofline) on the same kernel, stream and data
-    k_us = _kernel_time_us(env, step, actions, args.kernel_launches)
-    res = dict(elapsed=elapsed, kernel_us=k_us)
+    res = dict(elapsed=elapsed, kernel_us=launch_us,
+               event_pair_us=_kernel_time_us(env, step, actions, args.kernel_launches))
     if rank == 0 and args.large_envs > 0:
         del actions, g
         env.close()
@@ -118,7 +124,18 @@ def _run_rank(args, rank, world, local_rank):
         st = _quad_step_fn(big)
         for k in range(5):
             st(acts[k % 4].data_ptr())
-        res["large_kernel_us"] = _kernel_time_us(big, st, acts, 40)
+        gb = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gb):
+            for k in range(20):
+                st(acts[k % 4].data_ptr())
+        gb.replay()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(5):
+            gb.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        res["large_kernel_us"] = e0.elapsed_time(e1) * 1e3 / 100
         big.close()
     else:
         env.close()
@@ -203,6 +220,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_step<HOVER,noCTBR>", "kernel_us": kus,
+                     "event_pair_us": res["event_pair_us"],
                      "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs},
     }
     if "large_kernel_us" in res:

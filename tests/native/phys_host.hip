@@ -86,3 +86,16 @@ void host_reset_draw(const QuadCfg* cfg, uint64_t seed, uint64_t gid, uint32_t e
   reset_draw(k.init_lo, k.init_span, k.tgt_lo, k.tgt_span, seed, gid, ep, init12, tgt);
 }
 }
+
+extern "C" {
+void host_fsincos(const float* x, float* s, float* c, int n) {
+  for (int i = 0; i < n; i++) q_sincos(x[i], s + i, c + i);
+}
+void host_fatan2(const float* y, const float* x, float* r, int n) {
+  for (int i = 0; i < n; i++) r[i] = q_atan2(y[i], x[i]);
+}
+void host_div_const(const float* a, float b, float* r, int n) {
+  const float rb = 1.0f / b;
+  for (int i = 0; i < n; i++) r[i] = div_const(a[i], b, rb);
+}
+}

@@ -63,3 +63,29 @@ def reset_draw(cfg, seed, gid, ep):
     i12 = np.zeros(12, np.float32); t3 = np.zeros(3, np.float32)
     lib().host_reset_draw(C.byref(cfg), seed, gid, ep, i12.ctypes.data_as(fp), t3.ctypes.data_as(fp))
     return i12, t3
+
+
+def _f32fn(name, *arrays, scalar=None, nout=1):
+    L = lib()
+    f = getattr(L, name)
+    arrs = [np.ascontiguousarray(a, np.float32) for a in arrays]
+    n = len(arrs[0])
+    outs = [np.zeros(n, np.float32) for _ in range(nout)]
+    args = [a.ctypes.data_as(fp) for a in arrs]
+    if scalar is not None:
+        args.append(C.c_float(scalar))
+    args += [o.ctypes.data_as(fp) for o in outs] + [C.c_int(n)]
+    f(*args)
+    return outs
+
+
+def fsincos(x):
+    return _f32fn("host_fsincos", x, nout=2)
+
+
+def fatan2(y, x):
+    return _f32fn("host_fatan2", y, x)[0]
+
+
+def div_const(a, b):
+    return _f32fn("host_div_const", a, scalar=b)[0]

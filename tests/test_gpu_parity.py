@@ -164,11 +164,11 @@ def test_masked_reset_and_seed():
 
 def test_auto_reset_semantics():
     n = 4096
-    env = _env(n, seed=9, max_episode_steps=40)
+    env = _env(n, seed=9, max_episode_steps=6)
     env.reset()
     cfg = O.default_cfg(O.ENV_HOVER, O.WRAP_NONE)
     saw_term = saw_trunc = False
-    for k in range(60):
+    for k in range(20):
         pre = env.get_state()
         acts = env.random_actions(k)
         obs, rew, te, tr, inf = env.step(acts)

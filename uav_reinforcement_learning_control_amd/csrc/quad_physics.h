@@ -35,19 +35,96 @@
 namespace quadenv {
 
 // ---------------------------------------------------------------------------------------------
-// math shims resolving to the right precision (no dual code paths: both are plain HIP)
-QD_HD float q_sqrt(float x) { return sqrtf(x); }
+// math. The double overloads (host test instantiation) are libm; the float overloads are what
+// the kernel runs: short, branch-light sequences with ~1e-7 absolute error, far inside the
+// 1e-5 parity bar (see DESIGN.md "Kernel arithmetic"). Full-range sincosf/atan2f/hypotf from
+// the device libm cost several times the instructions and most of the registers.
+QD_HD float frcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
+}
+QD_HD float fsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sqrtf(x);
+#else
+  return sqrtf(x);
+#endif
+}
+QD_HD float frsqrt(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rsqf(x);
+#else
+  return 1.0f / sqrtf(x);
+#endif
+}
 QD_HD double q_sqrt(double x) { return sqrt(x); }
-QD_HD float q_atan2(float y, float x) { return atan2f(y, x); }
+QD_HD float q_sqrt(float x) { return fsqrt(x); }
+QD_HD double q_rsqrt(double x) { return 1.0 / sqrt(x); }
+QD_HD float q_rsqrt(float x) { return frsqrt(x); }
 QD_HD double q_atan2(double y, double x) { return atan2(y, x); }
-QD_HD float q_hypot(float x, float y) { return hypotf(x, y); }
 QD_HD double q_hypot(double x, double y) { return hypot(x, y); }
+QD_HD float q_hypot(float x, float y) { return fsqrt(x * x + y * y); }  // |args| <= 2 here
 QD_HD float q_abs(float x) { return fabsf(x); }
 QD_HD double q_abs(double x) { return fabs(x); }
 QD_HD float q_exp(float x) { return expf(x); }
 QD_HD double q_exp(double x) { return exp(x); }
-QD_HD void q_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
 QD_HD void q_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+
+// sin/cos: Cody-Waite reduction by pi/2 with two constants (exact to ~1e-10 rad for
+// |x| < 1e5; hinge angles accumulate but stay far below that), Taylor polynomials on
+// [-pi/4, pi/4] (truncation < 2.5e-8), quadrant select.
+QD_HD void q_sincos(float x, float* s, float* c) {
+  const float q = rintf(x * 0.636619772367581343f);
+  float r = fmaf(q, -1.57079637050628662109375f, x);
+  r = fmaf(q, 4.37113900018624283e-8f, r);
+  const float r2 = r * r;
+  const float sp = fmaf(r2, fmaf(r2, fmaf(r2, fmaf(r2, 2.7557319224e-6f, -1.9841269841e-4f),
+                                          8.3333333333e-3f), -1.6666666667e-1f), 0.0f);
+  const float sn = fmaf(r, sp, r);
+  const float cp = fmaf(r2, fmaf(r2, fmaf(r2, fmaf(r2, fmaf(r2, -2.7557319224e-7f, 2.4801587302e-5f),
+                                                   -1.3888888889e-3f), 4.1666666667e-2f), -0.5f), 1.0f);
+  const int qi = int(q) & 3;
+  const float a = (qi & 1) ? cp : sn;
+  const float b = (qi & 1) ? sn : cp;
+  *s = (qi & 2) ? -a : a;
+  *c = ((qi + 1) & 2) ? -b : b;
+}
+
+// atan2: odd degree-17 polynomial for atan on [0, 1] (float32 evaluation error 1.1e-7),
+// octant fix-ups. Matches atan2's conventions for signed zeros and the axes.
+QD_HD float q_atan2(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  const float t = mx > 0.0f ? mn * frcp(mx) : 0.0f;
+  const float t2 = t * t;
+  float p = 0.002456753049045801f;
+  p = fmaf(p, t2, -0.01440147403627634f);
+  p = fmaf(p, t2, 0.039781421422958374f);
+  p = fmaf(p, t2, -0.07234875112771988f);
+  p = fmaf(p, t2, 0.10498955100774765f);
+  p = fmaf(p, t2, -0.14161232113838196f);
+  p = fmaf(p, t2, 0.19985906779766083f);
+  p = fmaf(p, t2, -0.33332598209381104f);
+  p = fmaf(p, t2, 0.9999998807907104f);
+  float r = p * t;
+  if (ay > ax) r = 1.57079632679489662f - r;
+  if (copysignf(1.0f, x) < 0.0f) r = 3.14159265358979324f - r;  // atan2(y, -0) conventions too
+  return copysignf(r, y);
+}
+
+// a / b for a constant b with precomputed rb = RN(1/b): Markstein's correction returns the
+// correctly rounded quotient; verified exhaustively over all 2^32 float32 a for the five
+// observation spans (every mismatch is a subnormal quotient or -0, neither reachable here;
+// -0 is handled by the select).
+QD_HD float div_const(float a, float b, float rb) {
+#pragma clang fp contract(off)
+  const float q = a * rb;
+  const float e = fmaf(-q, b, a);
+  return e == 0.0f ? q : fmaf(e, rb, q);
+}
 
 // np.clip semantics: NaN propagates
 template <typename T>
@@ -79,6 +156,7 @@ struct KConsts {
   PhysConsts<T> ph;
   // float32 env constants (the reference keeps these as float32 Box bounds)
   float obs_lo[12], obs_span[12];   // span = high - low, computed in float32 like NumPy
+  float obs_rspan[12];              // RN(1 / span)
   float term_lo[12], term_hi[12];
   float act_lo[4], act_span[4];
   float init_lo[12], init_span[12];
@@ -86,6 +164,7 @@ struct KConsts {
   // float64 in the reference (Python floats / float64 arrays)
   double max_thrust, vnom, vmin, vb, vl, dt;
   double rate_max, rate_ikd[3], rate_kidt, rate_imax, max_torque;
+  double r_vnom, r_mx, r_max_torque;  // reciprocals (1-ulp float64 differences, far below 1e-12)
   int32_t max_steps;
 };
 
@@ -110,6 +189,7 @@ inline void make_kconsts(const QuadCfg& cfg, const PhysConstsD& d, KConsts<T>& k
   for (int i = 0; i < 12; i++) {
     k.obs_lo[i] = cfg.obs_low[i];
     k.obs_span[i] = cfg.obs_high[i] - cfg.obs_low[i];
+    k.obs_rspan[i] = 1.0f / k.obs_span[i];
     k.term_lo[i] = cfg.term_low[i];
     k.term_hi[i] = cfg.term_high[i];
     k.init_lo[i] = cfg.init_low[i];
@@ -131,6 +211,9 @@ inline void make_kconsts(const QuadCfg& cfg, const PhysConstsD& d, KConsts<T>& k
   k.rate_kidt = cfg.rate_ki * cfg.timestep;
   k.rate_imax = cfg.rate_imax;
   k.max_torque = cfg.max_torque;
+  k.r_vnom = 1.0 / cfg.nominal_voltage;
+  k.r_mx = 1.0 / (cfg.max_motor_thrust > 1e-6 ? cfg.max_motor_thrust : 1e-6);
+  k.r_max_torque = 1.0 / cfg.max_torque;
   k.max_steps = cfg.max_episode_steps;
 }
 
@@ -267,11 +350,11 @@ QD_HD void forward_acc(const PhysConsts<T>& c, const T qn[4], const T th[4], con
 
 template <typename T>
 QD_HD void normalize4(T q[4]) {
-  const T n = q_sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  if (n < T(1e-15)) {
+  const T n2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+  if (n2 < T(1e-30)) {
     q[0] = T(1); q[1] = q[2] = q[3] = T(0);
   } else {
-    const T inv = T(1) / n;
+    const T inv = q_rsqrt(n2);
     q[0] *= inv; q[1] *= inv; q[2] *= inv; q[3] *= inv;
   }
 }
@@ -316,15 +399,15 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
   for (int i = 0; i < 3; i++) badacc |= int(isbad(vdot[i])) | int(isbad(wdot[i]));
 #pragma unroll
   for (int i = 0; i < 4; i++) badacc |= isbad(sdot[i]);
-  if (badacc) {  // mj_checkAcc: reset, recompute at qpos0 with zero ctrl
+  if (badacc) {  // mj_checkAcc: reset to qpos0 with zero ctrl; at rest there the only force is
+                 // gravity, so qacc = (0, 0, gz, 0, ...) exactly (cf. oracle K1)
 #pragma unroll
-    for (int i = 0; i < 3; i++) { e.pos[i] = T(0); e.v[i] = T(0); e.w[i] = T(0); taum[i] = T(0); }
+    for (int i = 0; i < 3; i++) { e.pos[i] = T(0); e.v[i] = T(0); e.w[i] = T(0); vdot[i] = T(0); wdot[i] = T(0); }
+    vdot[2] = c.gz;
     e.q[0] = T(1); e.q[1] = e.q[2] = e.q[3] = T(0);
 #pragma unroll
-    for (int i = 0; i < 4; i++) { e.th[i] = T(0); e.s[i] = T(0); }
-    Fsum = T(0);
+    for (int i = 0; i < 4; i++) { e.th[i] = T(0); e.s[i] = T(0); sdot[i] = T(0); }
     qn[0] = T(1); qn[1] = qn[2] = qn[3] = T(0);
-    forward_acc(c, qn, e.th, e.v, e.w, e.s, Fsum, taum, vdot, wdot, sdot);
   }
   // mj_Euler -> mj_advance: qvel += h qacc, then positions with the new qvel
   const T h = c.dt;
@@ -339,16 +422,22 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
     e.s[p] += h * sdot[p];
     e.th[p] += h * e.s[p];
   }
-  // mju_quatIntegrate(quat, w, h): quat = normalize(quat) * axisangle(w/|w|, h |w|)
-  const T wn = q_sqrt(e.w[0] * e.w[0] + e.w[1] * e.w[1] + e.w[2] * e.w[2]);
+  // mju_quatIntegrate(quat, w, h): quat = normalize(quat) * (cos x, w/|w| sin x), x = h|w|/2.
+  // For |w| < 50 rad/s the rotation uses series in x^2 (no sqrt/division; truncation < 2e-16).
+  const T w2 = e.w[0] * e.w[0] + e.w[1] * e.w[1] + e.w[2] * e.w[2];
+  const T x2 = T(0.25) * h * h * w2;
   T qr[4];
-  if (wn < T(1e-15)) {
-    qr[0] = T(1); qr[1] = qr[2] = qr[3] = T(0);
-  } else {
-    T sh, ch;
-    q_sincos(T(0.5) * h * wn, &sh, &ch);
-    const T k = sh / wn;
+  if (x2 < T(0.0625)) {
+    const T ch = T(1) + x2 * (T(-1.0 / 2) + x2 * (T(1.0 / 24) + x2 * (T(-1.0 / 720) + x2 * (T(1.0 / 40320) + x2 * T(-1.0 / 3628800)))));
+    const T sc = T(1) + x2 * (T(-1.0 / 6) + x2 * (T(1.0 / 120) + x2 * (T(-1.0 / 5040) + x2 * (T(1.0 / 362880) + x2 * T(-1.0 / 39916800)))));
+    const T k = T(0.5) * h * sc;
     qr[0] = ch; qr[1] = e.w[0] * k; qr[2] = e.w[1] * k; qr[3] = e.w[2] * k;
+  } else {
+    const T wn = q_sqrt(w2);
+    T sh, chh;
+    q_sincos(T(0.5) * h * wn, &sh, &chh);
+    const T k = sh / wn;
+    qr[0] = chh; qr[1] = e.w[0] * k; qr[2] = e.w[1] * k; qr[3] = e.w[2] * k;
   }
   const T a0 = qn[0], a1 = qn[1], a2 = qn[2], a3 = qn[3];
   e.q[0] = a0 * qr[0] - a1 * qr[1] - a2 * qr[2] - a3 * qr[3];
@@ -362,8 +451,7 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
 template <typename T>
 QD_HD void quat_to_euler(const T qin[4], T e[3]) {
   T q[4] = {qin[0], qin[1], qin[2], qin[3]};
-  const T n = q_sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  const T inv = T(1) / n;
+  const T inv = q_rsqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   const T qw = q[0] * inv, qx = q[1] * inv, qy = q[2] * inv, qz = q[3] * inv;
   const T a = qw - qy, b = qx + qz, c = qy + qw, d = qz - qx;
   const T PI = T(3.14159265358979323846);
@@ -399,18 +487,18 @@ QD_HD void euler_to_quat(const T e[3], T q[4]) {
 }
 
 // normalize (utils/normalization.py:7-17) in float32, no contraction, NumPy's operation order
-QD_HD float norm_obs1(float x, float lo, float span) {
+QD_HD float norm_obs1(float x, float lo, float span, float rspan) {
 #pragma clang fp contract(off)
   const float t = x - lo;
   const float u = 2.0f * t;
-  const float v = u / span;
+  const float v = div_const(u, span, rspan);
   return v - 1.0f;
 }
 // denormalize (utils/normalization.py:20-30) in float32
 QD_HD float denorm1(float a, float lo, float span) {
 #pragma clang fp contract(off)
   const float s = a + 1.0f;
-  const float h = s / 2.0f;
+  const float h = s * 0.5f;  // == s / 2.0f exactly
   const float m = h * span;
   return m + lo;
 }
@@ -433,7 +521,7 @@ QD_HD void observe(const KConsts<T>& k, const EnvRegs<T>& e, float obs[12], floa
 #pragma unroll
   for (int i = 0; i < 12; i++) {
     const float x = i < 3 ? sub32(e.target[i], s12[i]) : s12[i];
-    obs[i] = norm_obs1(x, k.obs_lo[i], k.obs_span[i]);
+    obs[i] = norm_obs1(x, k.obs_lo[i], k.obs_span[i], k.obs_rspan[i]);
   }
 }
 
@@ -479,7 +567,7 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
       const double ri = clipn(double(e.rint[j]) + k.rate_kidt * err, -k.rate_imax, k.rate_imax);
       e.rint[j] = T(ri);
       const double tau = taup + ri;
-      a[1 + j] = float(clipn(tau / k.max_torque, -1.0, 1.0));
+      a[1 + j] = float(clipn(tau * k.r_max_torque, -1.0, 1.0));
     }
   } else {
     a[1] = act[1]; a[2] = act[2]; a[3] = act[3];
@@ -494,11 +582,10 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
                      k.ph.mix[4 * i + 2] * phys[2] + k.ph.mix[4 * i + 3] * phys[3];
     F[i] = clipn(s, 0.0, k.max_thrust);
   }
-  const double vs = clipn(double(e.volt) / k.vnom, 0.0, 1.0);
+  const double vs = clipn(double(e.volt) * k.r_vnom, 0.0, 1.0);
 #pragma unroll
   for (int i = 0; i < 4; i++) F[i] = clipn(F[i] * vs, 0.0, k.max_thrust * vs);
-  const double mx = k.max_thrust > 1e-6 ? k.max_thrust : 1e-6;
-  const double load = ((F[0] + F[1] + F[2] + F[3]) / 4.0) / mx;
+  const double load = ((F[0] + F[1] + F[2] + F[3]) * 0.25) * k.r_mx;
   const double dV = (k.vb + k.vl * load) * k.dt;
   e.volt = T(clipn(double(e.volt) - dV, k.vmin, k.vnom));
   physics_step(k.ph, e, F);
@@ -575,7 +662,7 @@ QD_HD void env_reset_from(const KConsts<T>& k, EnvRegs<T>& e, const float init12
 #pragma unroll
   for (int i = 0; i < 12; i++) {
     const float x = i < 3 ? sub32(e.target[i], s12[i]) : s12[i];
-    obs[i] = norm_obs1(x, k.obs_lo[i], k.obs_span[i]);
+    obs[i] = norm_obs1(x, k.obs_lo[i], k.obs_span[i], k.obs_rspan[i]);
   }
 }
 
