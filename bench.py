@@ -114,6 +114,8 @@ def _run_rank(args, rank, world, local_rank):
     # per-launch kernel time (roofline) on the same kernel, stream and data
     res = dict(elapsed=elapsed, kernel_us=launch_us,
                event_pair_us=_kernel_time_us(env, step, actions, args.kernel_launches))
+    if args.rollout_steps > 0:
+        res["rollout"] = _rollout_phase(env, args)
     if rank == 0 and args.large_envs > 0:
         del actions, g
         env.close()
@@ -140,6 +142,23 @@ def _run_rank(args, rank, world, local_rank):
     else:
         env.close()
     return res
+
+
+def _rollout_phase(env, args) -> dict:
+    """PPO rollout phase on the same 65,536 envs: policy MLP forward (actor + critic, 2x128),
+    Gaussian sample, clip, env step, TimeLimit bootstrap, buffer writes -- one hipGraph per
+    rollout step -- plus the GAE kernel, timed over n_steps."""
+    from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
+    m = PPO(env, PPOConfig(n_steps=args.rollout_steps), seed=0)
+    m.collect_rollouts(use_graph=True)  # capture + warm
+    rs = m.collect_rollouts(use_graph=True)
+    out = {"env_steps_per_s": rs.env_steps / rs.seconds, "n_steps": args.rollout_steps,
+           "ms_per_step": rs.seconds / args.rollout_steps * 1e3,
+           "what": "policy fwd (actor+critic MLP 12-128-128, fp32) + sample + env step + buffers, "
+                   "graph-replayed; GAE included"}
+    del m
+    torch.cuda.empty_cache()
+    return out
 
 
 def _cpu_baseline(seconds: float) -> dict:
@@ -185,6 +204,7 @@ def main():
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--large-envs", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--rollout-steps", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -223,6 +243,8 @@ def main():
                      "event_pair_us": res["event_pair_us"],
                      "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs},
     }
+    if "rollout" in res:
+        line["rollout_phase"] = res["rollout"]
     if "large_kernel_us" in res:
         lk = res["large_kernel_us"]
         line["large_batch"] = {"envs": args.large_envs, "kernel_us": lk,

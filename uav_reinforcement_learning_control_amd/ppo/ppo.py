@@ -50,6 +50,38 @@ class PPOConfig:
     adam_eps: float = 1e-5
 
 
+def ppo_loss(policy: ActorCritic, obs, act, logp_old, adv, ret, cfg: PPOConfig):
+    """SB3 PPO.train minibatch loss: returns (loss, pg_loss, vf_loss, entropy, clip_fraction)."""
+    mean, v = policy.forward_heads(obs)
+    logp = policy.log_prob(mean, act)
+    if cfg.normalize_advantage and adv.numel() > 1:
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    ratio = torch.exp(logp - logp_old)
+    pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - cfg.clip_range, 1 + cfg.clip_range)).mean()
+    vf = nn.functional.mse_loss(ret, v)
+    ent = policy.entropy()
+    loss = pg + cfg.ent_coef * (-ent) + cfg.vf_coef * vf
+    clip_frac = ((ratio - 1).abs() > cfg.clip_range).float().mean()
+    return loss, pg, vf, ent, clip_frac
+
+
+def allreduce_mean_(params, flat: torch.Tensor, world: int) -> None:
+    """Average the gradients of `params` over ranks with ONE all_reduce of a flat fp32 bucket."""
+    grads = [p.grad for p in params]
+    off = 0
+    for g in grads:
+        k = g.numel()
+        flat[off:off + k].copy_(g.reshape(-1))
+        off += k
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    flat.div_(world)
+    off = 0
+    for g in grads:
+        k = g.numel()
+        g.copy_(flat[off:off + k].view_as(g))
+        off += k
+
+
 @dataclass
 class RolloutStats:
     episodes: int = 0
@@ -94,72 +126,86 @@ class PPO:
         else:
             self.batch = max(1, total // self.cfg.n_minibatches)
         self._flat = torch.zeros(sum(p.numel() for p in self.params), **f32)
+        self._t = torch.zeros(1, dtype=torch.long, device=self.device)
+        self._act_env = torch.zeros(n, 4, **f32)
+        self._done_stats = torch.zeros(3, dtype=torch.float64, device=self.device)
+        self._graph = None
 
     # ------------------------------------------------------------------------------------
     @torch.no_grad()
-    def collect_rollouts(self) -> RolloutStats:
+    def _rollout_step(self):
+        """One rollout step on static tensors; capturable into a hipGraph (no host sync).
+        Writes row t = self._t of the time-major buffers and advances self._t on the device."""
+        env, cfg, pol = self.env, self.cfg, self.policy
+        t = self._t
+        self.buf_obs.index_copy_(0, t, self.last_obs.unsqueeze(0))
+        self.buf_start.index_copy_(0, t, self.last_start.unsqueeze(0))
+        mean, v = pol.forward_heads(self.last_obs)
+        a = mean + pol.log_std.exp() * torch.randn_like(mean)
+        self.buf_act.index_copy_(0, t, a.unsqueeze(0))
+        self.buf_logp.index_copy_(0, t, pol.log_prob(mean, a).unsqueeze(0))
+        self.buf_val.index_copy_(0, t, v.unsqueeze(0))
+        torch.clamp(a, -1.0, 1.0, out=self._act_env)   # clipped only when sent to the env
+        obs, rew, term, trunc, info = env.step(self._act_env)
+        done = (term | trunc).float()
+        timeout = (trunc & ~term).float()
+        # TimeLimit bootstrap (SB3 collect_rollouts): r += gamma * V(terminal_obs)
+        tv = pol.value(info["terminal_observation"])
+        r = rew + cfg.gamma * timeout * torch.nan_to_num(tv)
+        self.buf_rew.index_copy_(0, t, r.unsqueeze(0))
+        # Monitor-style episode statistics (raw env reward)
+        self.ep_ret += rew
+        self.ep_len += 1
+        self._done_stats += torch.stack([(self.ep_ret * done).sum(), (self.ep_len * done).sum(),
+                                         done.sum()]).double()
+        self.ep_ret *= 1 - done
+        self.ep_len *= 1 - done
+        self.last_obs.copy_(obs)
+        self.last_start.copy_(done)
+        self._t += 1
+
+    def _capture(self):
+        # warm the kernels (rocBLAS handles, allocator) on a side stream, then capture one step
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._rollout_step()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._t.zero_()
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph):
+            self._rollout_step()
+        torch.cuda.synchronize(self.device)
+
+    @torch.no_grad()
+    def collect_rollouts(self, use_graph: bool = True) -> RolloutStats:
         env, cfg, pol = self.env, self.cfg, self.policy
         if not self._started:
             self.last_obs.copy_(env.reset())
             self.last_start.fill_(1.0)
             self._started = True
+            if use_graph:
+                self._capture()
         t0 = time.perf_counter()
-        done_ret = torch.zeros((), dtype=torch.float64, device=self.device)
-        done_len = torch.zeros((), dtype=torch.float64, device=self.device)
-        done_cnt = torch.zeros((), dtype=torch.float64, device=self.device)
-        for t in range(cfg.n_steps):
-            self.buf_obs[t].copy_(self.last_obs)
-            self.buf_start[t].copy_(self.last_start)
-            a, logp, v = pol.act(self.last_obs)
-            self.buf_act[t].copy_(a)
-            self.buf_logp[t].copy_(logp)
-            self.buf_val[t].copy_(v)
-            obs, rew, term, trunc, info = env.step(a.clamp(-1.0, 1.0).contiguous())
-            done = term | trunc
-            timeout = (trunc & ~term).float()
-            # TimeLimit bootstrap (SB3 collect_rollouts): r += gamma * V(terminal_obs)
-            tv = pol.value(info["terminal_observation"])
-            r = rew + cfg.gamma * torch.where(timeout > 0, tv, torch.zeros_like(tv))
-            self.buf_rew[t].copy_(r)
-            # Monitor-style episode statistics (raw env reward)
-            self.ep_ret += rew
-            self.ep_len += 1
-            df = done.float()
-            done_ret += (self.ep_ret * df).sum()
-            done_len += (self.ep_len * df).sum()
-            done_cnt += df.sum()
-            self.ep_ret *= 1 - df
-            self.ep_len *= 1 - df
-            self.last_obs.copy_(obs)
-            self.last_start.copy_(df)
+        self._t.zero_()
+        self._done_stats.zero_()
+        for _ in range(cfg.n_steps):
+            if use_graph and self._graph is not None:
+                self._graph.replay()
+            else:
+                self._rollout_step()
         last_v = pol.value(self.last_obs)
         gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
             cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
         torch.cuda.synchronize(self.device)
         steps = cfg.n_steps * env.num_envs
         self.num_timesteps += steps * self.world
-        c = float(done_cnt.item())
-        return RolloutStats(episodes=int(c),
-                            mean_return=float(done_ret.item() / c) if c else float("nan"),
-                            mean_length=float(done_len.item() / c) if c else float("nan"),
+        ret_sum, len_sum, c = self._done_stats.tolist()
+        return RolloutStats(episodes=int(c), mean_return=ret_sum / c if c else float("nan"),
+                            mean_length=len_sum / c if c else float("nan"),
                             env_steps=steps, seconds=time.perf_counter() - t0)
 
     # ------------------------------------------------------------------------------------
-    def _allreduce_grads(self):
-        grads = [p.grad for p in self.params]
-        off = 0
-        for g in grads:
-            k = g.numel()
-            self._flat[off:off + k].copy_(g.view(-1))
-            off += k
-        dist.all_reduce(self._flat, op=dist.ReduceOp.SUM)
-        self._flat.div_(self.world)
-        off = 0
-        for g in grads:
-            k = g.numel()
-            g.view(-1).copy_(self._flat[off:off + k])
-            off += k
-
     def train(self, n_epochs: Optional[int] = None, max_minibatches: Optional[int] = None) -> dict:
         cfg, pol = self.cfg, self.policy
         total = cfg.n_steps * self.env.num_envs
@@ -179,26 +225,17 @@ class PPO:
                 if max_minibatches is not None and done >= max_minibatches:
                     break
                 idx = perm[m * B:(m + 1) * B]
-                mean, v = pol.forward_heads(obs[idx])
-                logp = pol.log_prob(mean, act[idx])
-                adv = adv_all[idx]
-                if cfg.normalize_advantage and B > 1:
-                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-                ratio = torch.exp(logp - logp_old[idx])
-                pg = -torch.min(adv * ratio,
-                                adv * torch.clamp(ratio, 1 - cfg.clip_range, 1 + cfg.clip_range)).mean()
-                vf = nn.functional.mse_loss(ret[idx], v)
-                ent = pol.entropy()
-                loss = pg + cfg.ent_coef * (-ent) + cfg.vf_coef * vf
+                loss, pg, vf, ent, cf = ppo_loss(pol, obs[idx], act[idx], logp_old[idx],
+                                                 adv_all[idx], ret[idx], cfg)
                 self.opt.zero_grad(set_to_none=False)
                 loss.backward()
                 if self.world > 1:
-                    self._allreduce_grads()
+                    allreduce_mean_(self.params, self._flat, self.world)
                 nn.utils.clip_grad_norm_(self.params, cfg.max_grad_norm)
                 self.opt.step()
                 with torch.no_grad():
-                    acc += torch.stack([pg.detach().double(), vf.detach().double(), ent.detach().double(),
-                                        ((ratio - 1).abs() > cfg.clip_range).float().mean().double()])
+                    acc += torch.stack([pg.detach().double(), vf.detach().double(),
+                                        ent.detach().double(), cf.double()])
                 done += 1
         a = (acc / max(done, 1)).tolist()
         stats.update(pg_loss=a[0], vf_loss=a[1], entropy=a[2], clip_fraction=a[3], n=done)
