@@ -125,6 +125,12 @@ int quad_reset(QuadHandle* h, const uint8_t* mask, float* obs, void* stream);
  * (the CTBR wrapper's rate space when wrapper == QUAD_WRAP_CTBR). Not clipped by the env. */
 int quad_step(QuadHandle* h, const float* actions, const QuadStepOut* out, void* stream);
 
+/* quad_step restricted to envs [first, first + count): rows of actions/out outside the range are
+ * neither read nor written. Sub-ranges on different streams let independent halves of a batch
+ * overlap (one half's physics with the other half's memory traffic, or with a policy kernel). */
+int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* actions,
+                    const QuadStepOut* out, void* stream);
+
 /* HoverEnv._get_obs for the current state (e.g. after quad_set_state). obs: device [N,12];
  * state12 (device [N,12] or NULL): the absolute QuadState vector (HoverEnv._state.vec()). */
 int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream);

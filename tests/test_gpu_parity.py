@@ -78,8 +78,16 @@ def _gpu_step(env, st, acts):
                 vscale=inf["voltage_scale"].cpu().numpy(), **g)
 
 
+@pytest.fixture(params=["1", "2", "4", "0"])
+def kernel_variant(request, monkeypatch):
+    """Every step kernel form must be exact: k_step_g with 1 (default), 2 or 4 lanes per env,
+    and the legacy one-thread-per-env k_step with an LDS obs transpose (QUADENV_LANES=0)."""
+    monkeypatch.setenv("QUADENV_LANES", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("env_name,wrapper,kind,wrap", VARIANTS)
-def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap):
+def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap, kernel_variant):
     n = 3000
     rng = np.random.default_rng(17 + kind * 2 + wrap)
     st = _random_states(n, rng)
@@ -107,7 +115,7 @@ def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap):
 @pytest.mark.parametrize("name,kind,wrap,ms", [("hover_steps", 0, 0, None), ("hover_trunc", 0, 0, 15),
                                                ("hover_nan", 0, 0, None), ("ctbr_steps", 0, 1, None),
                                                ("traj_ctbr_steps", 1, 1, None), ("traj_steps", 1, 0, None)])
-def test_step_matches_reference_goldens(golden_dir, name, kind, wrap, ms):
+def test_step_matches_reference_goldens(golden_dir, name, kind, wrap, ms, kernel_variant):
     d = np.load(os.path.join(golden_dir, f"golden_{name}.npz"))
     n = len(d["action"])
     env = _env(n, "trajectory" if kind else "hover", "RateControlWrapper" if wrap else None,
@@ -162,7 +170,7 @@ def test_masked_reset_and_seed():
     env.close()
 
 
-def test_auto_reset_semantics():
+def test_auto_reset_semantics(kernel_variant):
     n = 4096
     env = _env(n, seed=9, max_episode_steps=6)
     env.reset()
@@ -207,7 +215,7 @@ def test_random_actions_match_oracle():
     env.close()
 
 
-def test_nan_and_extreme_actions():
+def test_nan_and_extreme_actions(kernel_variant):
     n = 256
     rng = np.random.default_rng(3)
     st = _random_states(n, rng, wide=False)
@@ -282,3 +290,35 @@ def test_gae_matches_sb3_restatement():
     adv, ret = gae(c(rew), c(val), c(starts), c(last), c(dones), gamma, lam)
     np.testing.assert_allclose(adv.cpu().numpy(), adv_ref, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(ret.cpu().numpy(), adv_ref + val, rtol=1e-4, atol=1e-4)
+
+
+def test_step_range_touches_only_its_rows(kernel_variant):
+    """quad_step_range(first, count): rows outside the range are neither read nor written, and the
+    two halves stepped separately equal one full step."""
+    import ctypes as C
+    from uav_reinforcement_learning_control_amd import _native as N
+    n = 3000
+    a = _env(n, seed=4)
+    b = _env(n, seed=4)
+    a.reset(); b.reset()
+    acts = a.random_actions(0)
+    oa, ra, ta, ua, _ = a.step(acts)
+    oa, ra, ta, ua = oa.clone(), ra.clone(), ta.clone(), ua.clone()
+    sentinel = torch.full((n, 12), 7.0, device="cuda:0")
+    b.obs.copy_(sentinel)
+    out = N.QuadStepOut(obs=b.obs.data_ptr(), reward=b.reward.data_ptr(),
+                        terminated=b.terminated.data_ptr(), truncated=b.truncated.data_ptr(),
+                        terminal_obs=b.terminal_obs.data_ptr())
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    N.check(N.lib().quad_step_range(b._h, 0, 1234, C.c_void_p(acts.data_ptr()), C.byref(out), s), "r")
+    torch.cuda.synchronize()
+    assert torch.equal(b.obs[1234:], sentinel[1234:])
+    N.check(N.lib().quad_step_range(b._h, 1234, n - 1234, C.c_void_p(acts.data_ptr()), C.byref(out), s), "r")
+    torch.cuda.synchronize()
+    assert torch.equal(b.obs, oa) and torch.equal(b.reward, ra)
+    assert torch.equal(b.terminated, ta) and torch.equal(b.truncated, ua)
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+    assert N.lib().quad_step_range(b._h, n - 1, 2, C.c_void_p(acts.data_ptr()), C.byref(out), s) == N.QUAD_EINVAL
+    a.close(); b.close()

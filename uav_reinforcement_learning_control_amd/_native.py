@@ -52,7 +52,7 @@ class QuadStepOut(C.Structure):
 
 # every symbol include/quadenv.h declares (checked by tests/test_abi.py)
 EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_create",
-           "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_observe",
+           "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
            "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae")
 
 
@@ -76,12 +76,13 @@ def _declare(L):
     L.quad_seed.argtypes = [vp, u64, vp]
     L.quad_reset.argtypes = [vp, vp, vp, vp]
     L.quad_step.argtypes = [vp, vp, C.POINTER(QuadStepOut), vp]
+    L.quad_step_range.argtypes = [vp, i32, i32, vp, C.POINTER(QuadStepOut), vp]
     L.quad_observe.argtypes = [vp, vp, vp, vp]
     L.quad_random_actions.argtypes = [vp, u32, vp, vp]
     L.quad_get_state.argtypes = [vp, C.POINTER(QuadStateSoA), i32, vp]
     L.quad_set_state.argtypes = [vp, C.POINTER(QuadStateSoA), i32, vp]
     L.quad_gae.argtypes = [vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
-    for n in ("quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_observe",
+    for n in ("quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae"):
         getattr(L, n).restype = C.c_int
 

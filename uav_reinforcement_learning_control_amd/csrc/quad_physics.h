@@ -131,10 +131,10 @@ template <typename T>
 QD_HD T clipn(T x, T lo, T hi) {
   return (x != x) ? x : (x < lo ? lo : (x > hi ? hi : x));
 }
-// mju_isBad
+// mju_isBad: NaN or |x| > 1e10 (one compare with an abs modifier)
 template <typename T>
 QD_HD bool isbad(T x) {
-  return !(x == x) || x > T(1e10) || x < T(-1e10);
+  return !(q_abs(x) <= T(1e10));
 }
 
 // ---------------------------------------------------------------------------------------------

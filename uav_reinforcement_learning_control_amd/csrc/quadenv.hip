@@ -17,11 +17,13 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
 
 #include "../../include/quadenv.h"
+#include "quad_lanes.h"
 #include "quad_model.h"
 #include "quad_physics.h"
 
@@ -53,7 +55,9 @@ struct KParams {
   float* soa;
   int32_t* step;
   uint32_t* ep;
-  int32_t n;
+  int32_t n;      // envs in the handle (SoA stride)
+  int32_t first;  // step launches cover envs [first, first + count)
+  int32_t count;
   int32_t auto_reset;
   uint64_t seed;
   uint64_t gid_base;
@@ -145,10 +149,10 @@ template <int KIND, bool CTBR>
 __global__ __launch_bounds__(BLOCK) void k_step(KParams p, const float4* __restrict__ act,
                                                 QuadStepOut out) {
   __shared__ float4 lds[BLOCK * 3];
-  const int block_first = blockIdx.x * BLOCK;
+  const int block_first = p.first + blockIdx.x * BLOCK;
   const int i = block_first + threadIdx.x;
   float obs[12];
-  if (i < p.n) {
+  if (i < p.first + p.count) {
     EnvRegs<float> e;
     load_env(p, i, e, CTBR);
     const float4 a4 = act[i];
@@ -177,7 +181,428 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, const float4* __restr
     }
     store_env(p, i, e, CTBR);
   }
-  store_obs_rows(lds, obs, out.obs, block_first, p.n);
+  store_obs_rows(lds, obs, out.obs, block_first, p.first + p.count);
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// k_step_g<KIND, CTBR, G>: the step with one env per GROUP of G lanes (G = 1, 2, 4; 64/G envs
+// per wave). Work that is a loop over 4 items in the one-thread form -- the props (hinge state and
+// inertia-box drag), the three atan2 of scipy's Euler algorithm, the four obs triples, the four
+// Philox blocks of the reset draw, the three half-angle sincos of from_euler -- is spread over the
+// group (lane l takes items l, l+G, ...); the rest is evaluated by every lane of the group (one
+// wave-instruction either way). Group reductions / broadcasts are DPP quad_perm (quad_lanes.h).
+// Why: at 65,536 envs the G = 1 form is one lone wave per SIMD (issue-latency bound); G > 1 buys
+// waves per SIMD at the price of the replicated part -- see DESIGN.md "Lane groups".
+template <int G, typename T>
+__device__ __forceinline__ T grp_pick(int m, const T* v) {  // v[m], m lane-dependent, m < 4
+  return pick4(m, v[0], v[1], v[2], v[3]);
+}
+
+template <int KIND, bool CTBR, int G>
+__global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __restrict__ act,
+                                                  QuadStepOut out) {
+  constexpr int NI = 4 / G;  // items per lane
+  const unsigned i_raw = unsigned(p.first) + (blockIdx.x * BLOCK + threadIdx.x) / G;
+  const int l = G == 1 ? 0 : int(threadIdx.x & (G - 1));
+  // G > 1: whole groups leave together. G = 1 keeps every thread (the LDS obs stage has a
+  // block barrier); out-of-range threads recompute the last env and store nothing.
+  const unsigned end = unsigned(p.first + p.count);
+  if (G > 1 && i_raw >= end) return;
+  const bool live = i_raw < end;
+  const unsigned i = live ? i_raw : end - 1;
+  const KConsts<float>& k = p.k;
+  const PhysConsts<float>& c = k.ph;
+  const size_t n = size_t(p.n);
+  const float* __restrict__ S = p.soa;
+  // ---- load: shared fields by every lane; per-prop / per-axis fields by their owner lane
+  float pos[3], q[4], v[3], w[3], tgt[3];
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    pos[j] = (S + (F_QPOS + j) * n)[i];
+    v[j] = (S + (F_QVEL + j) * n)[i];
+    w[j] = (S + (F_QVEL + 3 + j) * n)[i];
+    tgt[j] = (S + (F_TGT + j) * n)[i];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) q[j] = (S + (F_QPOS + 3 + j) * n)[i];
+  float volt = (S + F_VOLT * n)[i];
+  int step = p.step[i];
+  const uint32_t ep = p.ep[i];  // prefetched: the reset branch must not add a dependent load
+  float th[NI], sp[NI];
+#pragma unroll
+  for (int it = 0; it < NI; it++) {
+    const int pr = l + it * G;
+    th[it] = (S + (F_QPOS + 7 + pr) * n)[i];
+    sp[it] = (S + (F_QVEL + 6 + pr) * n)[i];
+  }
+  float ri[3] = {0.f, 0.f, 0.f};
+  if (CTBR) {
+#pragma unroll
+    for (int j = 0; j < 3; j++) ri[j] = (S + (F_RINT + j) * n)[i];
+  }
+  const float4 a4 = act[i];
+  float a[4] = {a4.x, a4.y, a4.z, a4.w};
+
+  // ---- RateControlWrapper.action (float64): three axes, every lane (cheap, no reduction)
+  if (CTBR) {
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const double err = double(a[1 + j]) * k.rate_max - double(w[j]);
+      const double rid = clipn(double(ri[j]) + k.rate_kidt * err, -k.rate_imax, k.rate_imax);
+      ri[j] = float(rid);
+      a[1 + j] = float(clipn((k.rate_ikd[j] * err + rid) * k.r_max_torque, -1.0, 1.0));
+    }
+  }
+  // ---- denormalize (float32) -> mixer, voltage sag, motor wrench (float64)
+  double phys[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) phys[j] = double(denorm1(a[j], k.act_lo[j], k.act_span[j]));
+  double F[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++)
+    F[r] = clipn(c.mix[4 * r] * phys[0] + c.mix[4 * r + 1] * phys[1] + c.mix[4 * r + 2] * phys[2] +
+                     c.mix[4 * r + 3] * phys[3], 0.0, k.max_thrust);
+  const double vs = clipn(double(volt) * k.r_vnom, 0.0, 1.0);
+#pragma unroll
+  for (int r = 0; r < 4; r++) F[r] = clipn(F[r] * vs, 0.0, k.max_thrust * vs);
+  volt = float(clipn(double(volt) - (k.vb + k.vl * (((F[0] + F[1] + F[2] + F[3]) * 0.25) * k.r_mx)) * k.dt,
+                     k.vmin, k.vnom));
+  // ---- mujoco.mj_step: mj_checkPos/Vel, bad ctrl
+  int bad = 0;
+#pragma unroll
+  for (int it = 0; it < NI; it++) bad |= int(isbad(th[it])) | int(isbad(sp[it]));
+#pragma unroll
+  for (int j = 0; j < 3; j++) bad |= int(isbad(pos[j])) | int(isbad(v[j])) | int(isbad(w[j]));
+#pragma unroll
+  for (int j = 0; j < 4; j++) bad |= int(isbad(q[j]));
+  bad = group_or<G>(bad);
+  int badctrl = bad;
+#pragma unroll
+  for (int r = 0; r < 4; r++) badctrl |= int(isbad(F[r]));
+  if (bad) {
+#pragma unroll
+    for (int j = 0; j < 3; j++) { pos[j] = 0.f; v[j] = 0.f; w[j] = 0.f; }
+    q[0] = 1.f; q[1] = q[2] = q[3] = 0.f;
+#pragma unroll
+    for (int it = 0; it < NI; it++) { th[it] = 0.f; sp[it] = 0.f; }
+  }
+  double Fc[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const double f = badctrl ? 0.0 : F[r];
+    Fc[r] = f < c.ctrl_lo ? c.ctrl_lo : (f > c.ctrl_hi ? c.ctrl_hi : f);
+  }
+  // ---- forward dynamics (forward_acc in quad_physics.h, props spread over the group)
+  float qn[4] = {q[0], q[1], q[2], q[3]};
+  normalize4(qn);
+  float R[9];
+  {
+    const float qw = qn[0], qx = qn[1], qy = qn[2], qz = qn[3];
+    R[0] = 1.f - 2.f * (qy * qy + qz * qz); R[1] = 2.f * (qx * qy - qw * qz); R[2] = 2.f * (qx * qz + qw * qy);
+    R[3] = 2.f * (qx * qy + qw * qz); R[4] = 1.f - 2.f * (qx * qx + qz * qz); R[5] = 2.f * (qy * qz - qw * qx);
+    R[6] = 2.f * (qx * qz - qw * qy); R[7] = 2.f * (qy * qz + qw * qx); R[8] = 1.f - 2.f * (qx * qx + qy * qy);
+  }
+  float vB[3];
+#pragma unroll
+  for (int j = 0; j < 3; j++) vB[j] = R[j] * v[0] + R[3 + j] * v[1] + R[6 + j] * v[2];
+  float FB[3] = {0.f, 0.f, 0.f}, tau[3] = {0.f, 0.f, 0.f}, Qs[NI], Qloc = 0.f, sloc = 0.f;
+#pragma unroll
+  for (int it = 0; it < NI; it++) {
+    const int pr = l + it * G;
+    const float pc[3] = {G == 1 ? c.pc[it][0] : pick4(pr, c.pc[0][0], c.pc[1][0], c.pc[2][0], c.pc[3][0]),
+                         G == 1 ? c.pc[it][1] : pick4(pr, c.pc[0][1], c.pc[1][1], c.pc[2][1], c.pc[3][1]),
+                         G == 1 ? c.pc[it][2] : pick4(pr, c.pc[0][2], c.pc[1][2], c.pc[2][2], c.pc[3][2])};
+    float sn, cs;
+    q_sincos(th[it], &sn, &cs);
+    float wxc[3];
+    cross(w, pc, wxc);
+    const float ub[3] = {vB[0] + wxc[0], vB[1] + wxc[1], vB[2] + wxc[2]};
+    const float wp[3] = {cs * w[0] + sn * w[1], -sn * w[0] + cs * w[1], w[2] + sp[it]};
+    const float up[3] = {cs * ub[0] + sn * ub[1], -sn * ub[0] + cs * ub[1], ub[2]};
+    float tp[3], fp[3];
+    box_drag(wp, up, c.p_kqa, c.p_kva, c.p_kql, c.p_kvl, tp, fp);
+    const float f[3] = {cs * fp[0] - sn * fp[1], sn * fp[0] + cs * fp[1], fp[2]};
+    const float t[3] = {cs * tp[0] - sn * tp[1], sn * tp[0] + cs * tp[1], tp[2]};
+    float rxf[3];
+    cross(pc, f, rxf);
+#pragma unroll
+    for (int j = 0; j < 3; j++) { FB[j] += f[j]; tau[j] += rxf[j] + t[j]; }
+    Qs[it] = tp[2];
+    Qloc += tp[2];
+    sloc += sp[it];
+  }
+#pragma unroll
+  for (int j = 0; j < 3; j++) { FB[j] = group_sum<G>(FB[j]); tau[j] = group_sum<G>(tau[j]); }
+  const float Qsum = group_sum<G>(Qloc), ssum = group_sum<G>(sloc);
+  {  // motor wrench (float64 -> float32), gravity at the system COM, base inertia-box drag
+    FB[2] += float(Fc[0] + Fc[1] + Fc[2] + Fc[3]);
+    tau[0] += float(c.syd[0] * Fc[0] + c.syd[1] * Fc[1] + c.syd[2] * Fc[2] + c.syd[3] * Fc[3]);
+    tau[1] += float(-(c.sxd[0] * Fc[0] + c.sxd[1] * Fc[1] + c.sxd[2] * Fc[2] + c.sxd[3] * Fc[3]));
+    tau[2] += float(c.g5d[0] * Fc[0] + c.g5d[1] * Fc[1] + c.g5d[2] * Fc[2] + c.g5d[3] * Fc[3]);
+    const float mg = c.mt * c.gz;
+    const float gB[3] = {mg * R[6], mg * R[7], mg * R[8]};
+    float tg[3];
+    cross(c.cbar, gB, tg);
+    float tb[3], fb[3];
+    box_drag(w, vB, c.b_kqa, c.b_kva, c.b_kql, c.b_kvl, tb, fb);
+#pragma unroll
+    for (int j = 0; j < 3; j++) { FB[j] += gB[j] + fb[j]; tau[j] += tg[j] + tb[j]; }
+  }
+  float vdot[3], wdot[3], sdot[NI];
+  {
+    float wc[3], wwc[3], fv[3], Iw[3], wIw[3], cxf[3], rhs[3], cxw[3], aB[3];
+    cross(w, c.cbar, wc);
+    cross(w, wc, wwc);
+#pragma unroll
+    for (int j = 0; j < 3; j++) fv[j] = FB[j] - c.mt * wwc[j];
+#pragma unroll
+    for (int j = 0; j < 3; j++) Iw[j] = c.IO[3 * j] * w[0] + c.IO[3 * j + 1] * w[1] + c.IO[3 * j + 2] * w[2];
+    cross(w, Iw, wIw);
+    cross(c.cbar, fv, cxf);
+    rhs[0] = tau[0] - wIw[0] - c.c_ax * ssum * w[1] - cxf[0];
+    rhs[1] = tau[1] - wIw[1] + c.c_ax * ssum * w[0] - cxf[1];
+    rhs[2] = tau[2] - wIw[2] - Qsum - cxf[2];
+#pragma unroll
+    for (int j = 0; j < 3; j++) wdot[j] = c.Ainv[3 * j] * rhs[0] + c.Ainv[3 * j + 1] * rhs[1] + c.Ainv[3 * j + 2] * rhs[2];
+    cross(c.cbar, wdot, cxw);
+#pragma unroll
+    for (int j = 0; j < 3; j++) aB[j] = fv[j] * c.inv_mt + cxw[j];
+#pragma unroll
+    for (int j = 0; j < 3; j++) vdot[j] = R[3 * j] * aB[0] + R[3 * j + 1] * aB[1] + R[3 * j + 2] * aB[2];
+#pragma unroll
+    for (int it = 0; it < NI; it++) sdot[it] = Qs[it] * c.inv_c_ax - wdot[2];
+  }
+  {  // mj_checkAcc: reset to qpos0; at rest there qacc is free fall
+    int badacc = 0;
+#pragma unroll
+    for (int it = 0; it < NI; it++) badacc |= int(isbad(sdot[it]));
+#pragma unroll
+    for (int j = 0; j < 3; j++) badacc |= int(isbad(vdot[j])) | int(isbad(wdot[j]));
+    if (group_or<G>(badacc)) {
+#pragma unroll
+      for (int j = 0; j < 3; j++) { pos[j] = 0.f; v[j] = 0.f; w[j] = 0.f; vdot[j] = 0.f; wdot[j] = 0.f; }
+      vdot[2] = c.gz;
+      qn[0] = 1.f; qn[1] = qn[2] = qn[3] = 0.f;
+#pragma unroll
+      for (int it = 0; it < NI; it++) { th[it] = 0.f; sp[it] = 0.f; sdot[it] = 0.f; }
+    }
+  }
+  // ---- mj_Euler: semi-implicit update, MuJoCo quaternion integration
+  const float h = c.dt;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    v[j] += h * vdot[j];
+    w[j] += h * wdot[j];
+    pos[j] += h * v[j];
+  }
+#pragma unroll
+  for (int it = 0; it < NI; it++) {
+    sp[it] += h * sdot[it];
+    th[it] += h * sp[it];
+  }
+  {
+    const float w2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    const float x2 = 0.25f * h * h * w2;
+    float qr[4];
+    if (x2 < 0.0625f) {
+      const float ch = 1.f + x2 * (-0.5f + x2 * (1.f / 24 + x2 * (-1.f / 720 + x2 * (1.f / 40320))));
+      const float sc = 1.f + x2 * (-1.f / 6 + x2 * (1.f / 120 + x2 * (-1.f / 5040 + x2 * (1.f / 362880))));
+      const float kk = 0.5f * h * sc;
+      qr[0] = ch; qr[1] = w[0] * kk; qr[2] = w[1] * kk; qr[3] = w[2] * kk;
+    } else {
+      const float wn = fsqrt(w2);
+      float sh, chh;
+      q_sincos(0.5f * h * wn, &sh, &chh);
+      const float kk = sh / wn;
+      qr[0] = chh; qr[1] = w[0] * kk; qr[2] = w[1] * kk; qr[3] = w[2] * kk;
+    }
+    q[0] = qn[0] * qr[0] - qn[1] * qr[1] - qn[2] * qr[2] - qn[3] * qr[3];
+    q[1] = qn[0] * qr[1] + qn[1] * qr[0] + qn[2] * qr[3] - qn[3] * qr[2];
+    q[2] = qn[0] * qr[2] - qn[1] * qr[3] + qn[2] * qr[0] + qn[3] * qr[1];
+    q[3] = qn[0] * qr[3] + qn[1] * qr[2] - qn[2] * qr[1] + qn[3] * qr[0];
+  }
+  step += 1;
+  // ---- QuadState (scipy as_euler('xyz')): items 0,1,2 = mid, half_sum, half_diff atan2
+  float s12[12];
+  {
+    const float inv = frsqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const float qw = q[0] * inv, qx = q[1] * inv, qy = q[2] * inv, qz = q[3] * inv;
+    const float A = qw - qy, B = qx + qz, Cc = qy + qw, D = qz - qx;
+    const float ys[4] = {q_hypot(Cc, D), B, D, D};
+    const float xs[4] = {q_hypot(A, B), A, Cc, Cc};
+    float at[3];
+    if constexpr (G == 1) {
+#pragma unroll
+      for (int m = 0; m < 3; m++) at[m] = q_atan2(ys[m], xs[m]);
+    } else if constexpr (G == 2) {
+      const float r0 = q_atan2(l ? ys[1] : ys[0], l ? xs[1] : xs[0]);  // items 0 | 1
+      const float r1 = q_atan2(ys[2], xs[2]);                           // item 2 (both lanes)
+      at[0] = group_bc<G, 0>(r0); at[1] = group_bc<G, 1>(r0); at[2] = r1;
+    } else {
+      const float r = q_atan2(grp_pick<G>(l, ys), grp_pick<G>(l, xs));
+      at[0] = group_bc<G, 0>(r); at[1] = group_bc<G, 1>(r); at[2] = group_bc<G, 2>(r);
+    }
+    const float PI = 3.14159265358979323846f;
+    const float mid = 2.f * at[0], hs = at[1], hd = at[2];
+    const bool case1 = fabsf(mid) <= 1e-7f, case2 = fabsf(mid - PI) <= 1e-7f;
+    float e[3];
+    if (!(case1 || case2)) { e[0] = hs - hd; e[2] = hs + hd; }
+    else { e[2] = 0.f; e[0] = case1 ? 2.f * hs : -2.f * hd; }
+    e[1] = mid - PI / 2.f;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      if (e[j] < -PI) e[j] += 2.f * PI;
+      else if (e[j] > PI) e[j] -= 2.f * PI;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) { s12[j] = pos[j]; s12[3 + j] = e[j]; s12[6 + j] = v[j]; s12[9 + j] = w[j]; }
+  }
+  const float reward = reward_of<float>(s12, tgt);
+  const bool term = terminated_of(k, s12);
+  const bool trunc = step >= k.max_steps;
+  // obs triples m = l + it*G (normalize, float32, correctly rounded)
+  float ob[NI][3];
+  auto obs_triples = [&](const float* st, const float* tg3) {
+#pragma unroll
+    for (int it = 0; it < NI; it++) {
+      const int m = l + it * G;
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        float x, lo, sp_, rs;
+        if constexpr (G == 1) {
+          x = st[3 * it + j]; lo = k.obs_lo[3 * it + j]; sp_ = k.obs_span[3 * it + j]; rs = k.obs_rspan[3 * it + j];
+        } else {
+          x = pick4(m, st[j], st[3 + j], st[6 + j], st[9 + j]);
+          lo = pick4(m, k.obs_lo[j], k.obs_lo[3 + j], k.obs_lo[6 + j], k.obs_lo[9 + j]);
+          sp_ = pick4(m, k.obs_span[j], k.obs_span[3 + j], k.obs_span[6 + j], k.obs_span[9 + j]);
+          rs = pick4(m, k.obs_rspan[j], k.obs_rspan[3 + j], k.obs_rspan[6 + j], k.obs_rspan[9 + j]);
+        }
+        if (m == 0) x = sub32(tg3[j], x);
+        ob[it][j] = norm_obs1(x, lo, sp_, rs);
+      }
+    }
+  };
+  obs_triples(s12, tgt);
+  if (l == 0 && live) {
+    out.reward[i] = reward;
+    out.terminated[i] = term;
+    out.truncated[i] = trunc;
+    if (out.voltage_scale) out.voltage_scale[i] = float(vs);
+    if (out.motor_commands)
+      reinterpret_cast<float4*>(out.motor_commands)[i] = make_float4(float(F[0]), float(F[1]), float(F[2]), float(F[3]));
+  }
+  if (out.state12 && live) {
+#pragma unroll
+    for (int it = 0; it < NI; it++) {
+      const int m = l + it * G;
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+        out.state12[size_t(i) * 12 + 3 * m + j] = G == 1 ? s12[3 * it + j] : pick4(m, s12[j], s12[3 + j], s12[6 + j], s12[9 + j]);
+    }
+  }
+  // ---- SB3 auto-reset (group-uniform branch)
+  const bool reset = (term || trunc) && p.auto_reset;
+  if (reset) {
+    if (out.terminal_obs && live) {
+#pragma unroll
+      for (int it = 0; it < NI; it++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) out.terminal_obs[size_t(i) * 12 + 3 * (l + it * G) + j] = ob[it][j];
+    }
+    const uint64_t gid = p.gid_base + uint64_t(i);
+    uint32_t r[NI][4];
+#pragma unroll
+    for (int it = 0; it < NI; it++) {  // Philox blocks l, l+G, ...
+      r[it][0] = uint32_t(gid); r[it][1] = uint32_t(gid >> 32); r[it][2] = ep; r[it][3] = uint32_t(l + it * G);
+      philox4x32_10(r[it], uint32_t(p.seed), uint32_t(p.seed >> 32));
+    }
+    uint32_t wd[15];  // word j of the 16-word draw lives in block j/4 -> lane (j/4)%G, item (j/4)/G
+#define QD_W(J) wd[J] = group_bcu<G, ((J) / 4) % G>(r[((J) / 4) / G][(J) % 4]);
+    QD_W(0) QD_W(1) QD_W(2) QD_W(3) QD_W(4) QD_W(5) QD_W(6) QD_W(7)
+    QD_W(8) QD_W(9) QD_W(10) QD_W(11) QD_W(12) QD_W(13) QD_W(14)
+#undef QD_W
+    float init12[12], tg[3];
+#pragma unroll
+    for (int j = 0; j < 12; j++) init12[j] = affine32(k.init_lo[j], u01(wd[j]), k.init_span[j]);
+#pragma unroll
+    for (int j = 0; j < 3; j++) tg[j] = affine32(k.tgt_lo[j], u01(wd[12 + j]), k.tgt_span[j]);
+    // from_euler: half-angle sincos of axes 0..2 spread over the group
+    float hsn[3], hcs[3];
+    if constexpr (G == 1) {
+#pragma unroll
+      for (int m = 0; m < 3; m++) q_sincos(init12[3 + m] * 0.5f, &hsn[m], &hcs[m]);
+    } else if constexpr (G == 2) {
+      float s0, c0;
+      q_sincos((l ? init12[4] : init12[3]) * 0.5f, &s0, &c0);
+      q_sincos(init12[5] * 0.5f, &hsn[2], &hcs[2]);
+      hsn[0] = group_bc<G, 0>(s0); hcs[0] = group_bc<G, 0>(c0);
+      hsn[1] = group_bc<G, 1>(s0); hcs[1] = group_bc<G, 1>(c0);
+    } else {
+      float s0, c0;
+      q_sincos(pick4(l, init12[3], init12[4], init12[5], init12[5]) * 0.5f, &s0, &c0);
+      hsn[0] = group_bc<G, 0>(s0); hcs[0] = group_bc<G, 0>(c0);
+      hsn[1] = group_bc<G, 1>(s0); hcs[1] = group_bc<G, 1>(c0);
+      hsn[2] = group_bc<G, 2>(s0); hcs[2] = group_bc<G, 2>(c0);
+    }
+    {
+      const float sr = hsn[0], cr = hcs[0], spp = hsn[1], cp = hcs[1], sy = hsn[2], cy = hcs[2];
+      q[0] = cy * cp * cr + sy * spp * sr;
+      q[1] = cy * cp * sr - sy * spp * cr;
+      q[2] = cy * spp * cr + sy * cp * sr;
+      q[3] = sy * cp * cr - cy * spp * sr;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      pos[j] = init12[j];
+      v[j] = init12[6 + j];
+      w[j] = init12[9 + j];
+      tgt[j] = KIND == QUAD_ENV_TRAJ ? init12[j] : tg[j];
+      ri[j] = 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < NI; it++) { th[it] = 0.f; sp[it] = 0.f; }
+    volt = float(k.vnom);
+    step = 0;
+    obs_triples(init12, tgt);  // QuadState round trip of the drawn state == the draw itself
+    if (l == 0 && live) p.ep[i] = ep + 1;
+  }
+  // ---- stores: obs rows. G = 1: staged through LDS so every wave-store writes 1 KiB
+  // contiguously; G > 1: one dwordx3 per lane, a wave's rows are already contiguous.
+  if constexpr (G == 1) {
+    __shared__ float4 lds[BLOCK * 3];
+    const float o12[12] = {ob[0][0], ob[0][1], ob[0][2], ob[1][0], ob[1][1], ob[1][2],
+                           ob[2][0], ob[2][1], ob[2][2], ob[3][0], ob[3][1], ob[3][2]};
+    store_obs_rows(lds, o12, out.obs, p.first + int(blockIdx.x) * BLOCK, int(end));
+  } else {
+#pragma unroll
+    for (int it = 0; it < NI; it++) {
+      float* o = out.obs + size_t(i) * 12 + 3 * (l + it * G);
+      o[0] = ob[it][0]; o[1] = ob[it][1]; o[2] = ob[it][2];
+    }
+  }
+  if (!live) return;
+  float* __restrict__ Sw = p.soa;
+#pragma unroll
+  for (int it = 0; it < NI; it++) {
+    const int pr = l + it * G;
+    (Sw + (F_QPOS + 7 + pr) * n)[i] = th[it];
+    (Sw + (F_QVEL + 6 + pr) * n)[i] = sp[it];
+  }
+  if (l == 0) {
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      (Sw + (F_QPOS + j) * n)[i] = pos[j];
+      (Sw + (F_QVEL + j) * n)[i] = v[j];
+      (Sw + (F_QVEL + 3 + j) * n)[i] = w[j];
+      if (reset) (Sw + (F_TGT + j) * n)[i] = tgt[j];  // the target only changes on reset
+      if (CTBR) (Sw + (F_RINT + j) * n)[i] = ri[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) (Sw + (F_QPOS + 3 + j) * n)[i] = q[j];
+    (Sw + F_VOLT * n)[i] = volt;
+    p.step[i] = step;
+  }
 }
 
 template <int KIND>
@@ -251,6 +676,7 @@ __global__ __launch_bounds__(BLOCK) void k_gae(const float* __restrict__ rew, co
 
 struct QuadHandle {
   QuadCfg cfg;
+  int lanes = 1;  // lanes per env in k_step_g (1, 2, 4); 0 = k_step. QUADENV_LANES overrides
   PhysConstsD pd;
   KParams kp;
   int device;
@@ -339,7 +765,8 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   if (!cfg || !out) return fail(QUAD_EINVAL, "cfg/out is NULL");
   *out = nullptr;
   if (n_envs <= 0) return fail(QUAD_EINVAL, "n_envs must be > 0");
-  if (int64_t(n_envs) * NF > int64_t(INT32_MAX)) return fail(QUAD_EINVAL, "n_envs too large");
+  if (int64_t(n_envs) * NF > int64_t(INT32_MAX) || int64_t(n_envs) * 4 > int64_t(INT32_MAX))
+    return fail(QUAD_EINVAL, "n_envs too large");
   if (cfg->env_kind != QUAD_ENV_HOVER && cfg->env_kind != QUAD_ENV_TRAJ)
     return fail(QUAD_EINVAL, "unknown env_kind");
   if (cfg->wrapper != QUAD_WRAP_NONE && cfg->wrapper != QUAD_WRAP_CTBR)
@@ -375,9 +802,18 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   h->kp.step = h->step;
   h->kp.ep = h->ep;
   h->kp.n = n_envs;
+  h->kp.first = 0;
+  h->kp.count = n_envs;
   h->kp.auto_reset = cfg->auto_reset;
   h->kp.seed = seed;
   h->kp.gid_base = env_id_base;
+  // measured on MI355X (DESIGN.md "Step-kernel forms"): the one-thread k_step is fastest while
+  // the batch is about one wave per SIMD; the k_step_g<1> form wins once waves queue up
+  h->lanes = n_envs < (1 << 18) ? 0 : 1;
+  if (const char* v = std::getenv("QUADENV_LANES")) {
+    const int g = std::atoi(v);
+    if (g == 0 || g == 1 || g == 2 || g == 4) h->lanes = g;
+  }
   *out = h;
   return QUAD_OK;
 }
@@ -414,7 +850,15 @@ int quad_reset(QuadHandle* h, const uint8_t* mask, float* obs, void* stream) {
 }
 
 int quad_step(QuadHandle* h, const float* actions, const QuadStepOut* out, void* stream) {
+  return quad_step_range(h, 0, h ? h->n : 0, actions, out, stream);
+}
+
+int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* actions,
+                    const QuadStepOut* out, void* stream) {
   if (!h || !actions || !out) return fail(QUAD_EINVAL, "handle/actions/out is NULL");
+  if (first < 0 || count < 0 || int64_t(first) + count > h->n)
+    return fail(QUAD_EINVAL, "env range out of bounds");
+  if (count == 0) return QUAD_OK;
   if (!out->obs || !out->reward || !out->terminated || !out->truncated)
     return fail(QUAD_EINVAL, "obs, reward, terminated and truncated are required");
   if ((reinterpret_cast<uintptr_t>(actions) | reinterpret_cast<uintptr_t>(out->obs)) & 15u)
@@ -423,17 +867,37 @@ int quad_step(QuadHandle* h, const float* actions, const QuadStepOut* out, void*
     return fail(QUAD_EINVAL, "motor_commands must be 16-byte aligned");
   DeviceGuard g(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 grid(grid_of(h->n)), blk(BLOCK);
   const float4* a = reinterpret_cast<const float4*>(actions);
   const bool traj = h->cfg.env_kind == QUAD_ENV_TRAJ, ctbr = h->cfg.wrapper == QUAD_WRAP_CTBR;
-  if (traj && ctbr)
-    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, h->kp, a, *out);
-  else if (traj)
-    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false>), grid, blk, 0, s, h->kp, a, *out);
-  else if (ctbr)
-    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true>), grid, blk, 0, s, h->kp, a, *out);
-  else
-    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false>), grid, blk, 0, s, h->kp, a, *out);
+  const dim3 blk(BLOCK);
+  const int G = h->lanes;
+  KParams kp = h->kp;
+  kp.first = first;
+  kp.count = count;
+  if (G == 0) {  // legacy one-thread-per-env form with the LDS obs transpose (A/B reference)
+    const dim3 grid(grid_of(count));
+    if (traj && ctbr)
+      hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, kp, a, *out);
+    else if (traj)
+      hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false>), grid, blk, 0, s, kp, a, *out);
+    else if (ctbr)
+      hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true>), grid, blk, 0, s, kp, a, *out);
+    else
+      hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false>), grid, blk, 0, s, kp, a, *out);
+  } else {
+    const dim3 grid(unsigned((int64_t(count) * G + BLOCK - 1) / BLOCK));
+#define QD_LAUNCH(GG)                                                                              \
+  if (traj && ctbr)                                                                             \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, true, GG>), grid, blk, 0, s, kp, a, *out);   \
+  else if (traj)                                                                                \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, false, GG>), grid, blk, 0, s, kp, a, *out);  \
+  else if (ctbr)                                                                                \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, true, GG>), grid, blk, 0, s, kp, a, *out);  \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG>), grid, blk, 0, s, kp, a, *out);
+    if (G == 1) { QD_LAUNCH(1) } else if (G == 2) { QD_LAUNCH(2) } else { QD_LAUNCH(4) }
+#undef QD_LAUNCH
+  }
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
 }
