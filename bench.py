@@ -145,19 +145,22 @@ def _run_rank(args, rank, world, local_rank):
 
 
 def _rollout_phase(env, args) -> dict:
-    """PPO rollout phase on the same 65,536 envs: policy MLP forward (actor + critic, 2x128),
-    Gaussian sample, clip, env step, TimeLimit bootstrap, buffer writes -- one hipGraph per
-    rollout step -- plus the GAE kernel, timed over n_steps."""
+    """PPO rollout phase on the same 65,536 envs, one hipGraph per rollout step, GAE included,
+    timed over n_steps: the MFMA policy path (policy kernel + env step + epilogue = 3 launches)
+    and, for comparison, the same step as torch ops on the same policy."""
     from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
-    m = PPO(env, PPOConfig(n_steps=args.rollout_steps), seed=0)
-    m.collect_rollouts(use_graph=True)  # capture + warm
-    rs = m.collect_rollouts(use_graph=True)
-    out = {"env_steps_per_s": rs.env_steps / rs.seconds, "n_steps": args.rollout_steps,
-           "ms_per_step": rs.seconds / args.rollout_steps * 1e3,
-           "what": "policy fwd (actor+critic MLP 12-128-128, fp32) + sample + env step + buffers, "
-                   "graph-replayed; GAE included"}
-    del m
-    torch.cuda.empty_cache()
+    out = {"n_steps": args.rollout_steps,
+           "what": "actor+critic MLP 12-128-128 fp32 + Gaussian sample + clip + env step + "
+                   "TimeLimit bootstrap + buffer rows, graph-replayed; GAE included"}
+    for name, fused in (("mfma", True), ("torch", False)):
+        m = PPO(env, PPOConfig(n_steps=args.rollout_steps, fused_policy=fused), seed=0)
+        m.collect_rollouts(use_graph=True)  # capture + warm
+        rs = m.collect_rollouts(use_graph=True)
+        out[name] = {"env_steps_per_s": rs.env_steps / rs.seconds,
+                     "ms_per_step": rs.seconds / args.rollout_steps * 1e3}
+        del m
+        torch.cuda.empty_cache()
+    out["env_steps_per_s"] = out["mfma"]["env_steps_per_s"]
     return out
 
 

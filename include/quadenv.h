@@ -153,6 +153,66 @@ int quad_gae(const float* rewards, const float* values, const float* episode_sta
              const float* last_values, const float* dones, int32_t T, int32_t N, float gamma,
              float gae_lambda, float* advantages, float* returns, void* stream);
 
+/* ---- Rollout policy on MFMA (row P): the SB3 ActorCritic that train.py:50-68 configures
+ * (MlpPolicy, net_arch pi=[128,128] vf=[128,128], ReLU, state-independent log_std), fp32.
+ * Parameter pointers are device fp32 in torch's nn.Linear layout ([out, in] row-major). */
+typedef struct QuadPolicyParams {
+  const float *pi_w0, *pi_b0, *pi_w1, *pi_b1;  /* mlp_extractor.policy_net.{0,2} [128,12] [128,128] */
+  const float *act_w, *act_b;                  /* action_net [4,128] [4] */
+  const float *vf_w0, *vf_b0, *vf_w1, *vf_b1;  /* mlp_extractor.value_net.{0,2} */
+  const float *val_w, *val_b;                  /* value_net [1,128] [1] */
+  const float* log_std;                        /* [4] */
+} QuadPolicyParams;
+
+/* Size (floats) of the packed policy image quad_policy_pack writes. */
+int32_t quad_policy_packed_floats(void);
+
+/* Repack the parameters into the MFMA fragment order the policy kernels read (call after every
+ * optimizer update that precedes a rollout; stream-ordered). `packed`: device, 16-byte aligned. */
+int quad_policy_pack(const QuadPolicyParams* p, float* packed, void* stream);
+
+/* One rollout-step policy evaluation (SB3 OnPolicyAlgorithm.collect_rollouts body):
+ * a = mean(obs) + exp(log_std) * z, z ~ N(0,1) from Philox(seed; env id, t, 0x200) + Box-Muller;
+ * actions_env = clip(a, -1, 1). t = *t_index (0 if NULL) is a running step counter (it is never
+ * reset, so successive rollouts draw fresh noise); row outputs go to row t % rows of time-major
+ * [rows,N,...] buffers; every row pointer may be NULL. */
+typedef struct QuadPolicyAct {
+  const float* obs;         /* [N,12] */
+  float* actions_env;       /* [N,4] clipped action for quad_step (16-byte aligned) */
+  float* actions;           /* [T,N,4] unclipped sample (rollout buffer) or NULL */
+  float* log_prob;          /* [T,N] or NULL */
+  float* value;             /* [T,N] critic V(obs) or NULL */
+  float* obs_copy;          /* [T,N,12] or NULL */
+  const float* last_start;  /* [N] episode_starts of this step or NULL */
+  float* episode_starts;    /* [T,N] or NULL */
+  const uint32_t* t_index;  /* device step counter or NULL */
+  int32_t rows;             /* T of the [T,N,...] buffers (>= 1) */
+  int32_t deterministic;    /* 1: a = mean (policy.predict(deterministic=True)) */
+  uint64_t seed;
+  uint64_t env_id_base;     /* global id of env 0 (keys the noise per env, shard-independent) */
+} QuadPolicyAct;
+int quad_policy_act(const float* packed, const QuadPolicyAct* a, int32_t n, void* stream);
+
+/* Rollout epilogue after quad_step for row t % rows, t = *t_index, then *t_index += 1:
+ * buf_rew[t] = reward + gamma * V(terminal_obs) where truncated && !terminated (TimeLimit
+ * bootstrap; the critic runs only on tiles that hold such an env); last_start = done;
+ * Monitor statistics: stats[0..2] += (sum of finished returns, lengths, count). */
+typedef struct QuadRolloutPost {
+  const float* reward;          /* [N] */
+  const uint8_t* terminated;    /* [N] */
+  const uint8_t* truncated;     /* [N] */
+  const float* terminal_obs;    /* [N,12] */
+  float* buf_rew;               /* [T,N] */
+  float* last_start;            /* [N] */
+  float* ep_ret;                /* [N] running episode return */
+  float* ep_len;                /* [N] running episode length */
+  double* stats;                /* [3] */
+  uint32_t* t_index;            /* device step counter */
+  int32_t rows;                 /* T of buf_rew */
+  float gamma;
+} QuadRolloutPost;
+int quad_rollout_post(const float* packed, const QuadRolloutPost* p, int32_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,13 +45,19 @@ int main(void) {{
   printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(QuadCfg), offsetof(QuadCfg, max_motor_thrust),
          offsetof(QuadCfg, viscosity), sizeof(QuadStepOut), offsetof(QuadStepOut, state12),
          sizeof(QuadStateSoA));
+  printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(QuadPolicyParams), sizeof(QuadPolicyAct),
+         offsetof(QuadPolicyAct, rows), offsetof(QuadPolicyAct, env_id_base),
+         sizeof(QuadRolloutPost), offsetof(QuadRolloutPost, rows), offsetof(QuadRolloutPost, gamma));
   return 0;
 }}''')
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(prog)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [C.sizeof(N.QuadCfg), N.QuadCfg.max_motor_thrust.offset, N.QuadCfg.viscosity.offset,
-            C.sizeof(N.QuadStepOut), N.QuadStepOut.state12.offset, C.sizeof(N.QuadStateSoA)]
+            C.sizeof(N.QuadStepOut), N.QuadStepOut.state12.offset, C.sizeof(N.QuadStateSoA),
+            C.sizeof(N.QuadPolicyParams), C.sizeof(N.QuadPolicyAct), N.QuadPolicyAct.rows.offset,
+            N.QuadPolicyAct.env_id_base.offset, C.sizeof(N.QuadRolloutPost),
+            N.QuadRolloutPost.rows.offset, N.QuadRolloutPost.gamma.offset]
     assert got == want
 
 

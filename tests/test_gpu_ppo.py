@@ -8,6 +8,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+FUSED = pytest.mark.parametrize("fused", [True, False], ids=["mfma", "torch"])
+
+
 def _ppo(n, T, **kw):
     from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
     from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
@@ -15,8 +18,9 @@ def _ppo(n, T, **kw):
     return PPO(env, PPOConfig(n_steps=T, **kw), seed=0)
 
 
-def test_graph_rollout_buffers_are_consistent():
-    m = _ppo(2048, 24, n_epochs=1, n_minibatches=4)
+@FUSED
+def test_graph_rollout_buffers_are_consistent(fused):
+    m = _ppo(2048, 24, n_epochs=1, n_minibatches=4, fused_policy=fused)
     rs = m.collect_rollouts(use_graph=True)
     rs = m.collect_rollouts(use_graph=True)
     with torch.no_grad():
@@ -30,17 +34,41 @@ def test_graph_rollout_buffers_are_consistent():
     # an episode start follows every done: starts are 0/1 and many episodes ended (random policy)
     st = m.buf_start.cpu().numpy()
     assert set(np.unique(st)) <= {0.0, 1.0} and rs.episodes > 0
-    assert m._t.item() == 24
+    assert (m._tc.item() == 48) if fused else (m._t.item() == 24)
+    # the obs rows chain: obs[t+1] of an env that did not finish is the env's next obs
+    assert torch.isfinite(m.buf_obs).all() and torch.all(m.buf_obs.abs() <= 1.0 + 1e-6)
 
 
-def test_eager_and_graph_rollouts_agree_on_semantics():
-    m = _ppo(1024, 8, n_epochs=1, n_minibatches=2)
+@FUSED
+def test_eager_and_graph_rollouts_agree_on_semantics(fused):
+    m = _ppo(1024, 8, n_epochs=1, n_minibatches=2, fused_policy=fused)
     m.collect_rollouts(use_graph=False)
-    assert m._t.item() == 8 and torch.isfinite(m.buf_ret).all()
+    assert ((m._tc.item() == 8) if fused else (m._t.item() == 8)) and torch.isfinite(m.buf_ret).all()
 
 
-def test_short_training_makes_progress():
-    m = _ppo(4096, 64, n_epochs=4, n_minibatches=8, learning_rate=3e-4)
+def test_fused_rollout_matches_replayed_env():
+    """Replay the fused rollout's unclipped actions through a fresh env with the same seed: the
+    rewards (after the TimeLimit bootstrap is removed), episode starts and obs rows must agree
+    bit for bit -- the epilogue only moves env outputs into the buffers."""
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    n, T = 512, 16
+    m = _ppo(n, T, n_epochs=1, n_minibatches=2, fused_policy=True)
+    m.collect_rollouts(use_graph=False)
+    env2 = QuadVecEnv(n, wrapper="RateControlWrapper", device="cuda:0", seed=3)
+    obs = env2.reset().clone()
+    start = torch.ones(n, device="cuda")
+    for t in range(T):
+        assert torch.equal(m.buf_obs[t], obs), t
+        assert torch.equal(m.buf_start[t], start), t
+        o, r, te, tr, info = env2.step(m.buf_act[t].clamp(-1, 1))
+        timeout = tr & ~te
+        assert torch.equal(m.buf_rew[t][~timeout], r[~timeout]), t
+        obs, start = o.clone(), (te | tr).float()
+
+
+@FUSED
+def test_short_training_makes_progress(fused):
+    m = _ppo(4096, 64, n_epochs=4, n_minibatches=8, learning_rate=3e-4, fused_policy=fused)
     lens = []
     for it in range(12):
         rs = m.collect_rollouts()

@@ -50,10 +50,32 @@ class QuadStepOut(C.Structure):
                 ("state12", C.c_void_p)]
 
 
+class QuadPolicyParams(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("pi_w0", "pi_b0", "pi_w1", "pi_b1", "act_w", "act_b",
+                                          "vf_w0", "vf_b0", "vf_w1", "vf_b1", "val_w", "val_b",
+                                          "log_std")]
+
+
+class QuadPolicyAct(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("actions_env", C.c_void_p), ("actions", C.c_void_p),
+                ("log_prob", C.c_void_p), ("value", C.c_void_p), ("obs_copy", C.c_void_p),
+                ("last_start", C.c_void_p), ("episode_starts", C.c_void_p),
+                ("t_index", C.c_void_p), ("rows", C.c_int32), ("deterministic", C.c_int32),
+                ("seed", C.c_uint64), ("env_id_base", C.c_uint64)]
+
+
+class QuadRolloutPost(C.Structure):
+    _fields_ = [("reward", C.c_void_p), ("terminated", C.c_void_p), ("truncated", C.c_void_p),
+                ("terminal_obs", C.c_void_p), ("buf_rew", C.c_void_p), ("last_start", C.c_void_p),
+                ("ep_ret", C.c_void_p), ("ep_len", C.c_void_p), ("stats", C.c_void_p),
+                ("t_index", C.c_void_p), ("rows", C.c_int32), ("gamma", C.c_float)]
+
+
 # every symbol include/quadenv.h declares (checked by tests/test_abi.py)
 EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_create",
            "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
-           "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae")
+           "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
+           "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post")
 
 
 class QuadError(RuntimeError):
@@ -82,8 +104,14 @@ def _declare(L):
     L.quad_get_state.argtypes = [vp, C.POINTER(QuadStateSoA), i32, vp]
     L.quad_set_state.argtypes = [vp, C.POINTER(QuadStateSoA), i32, vp]
     L.quad_gae.argtypes = [vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp, vp]
+    L.quad_policy_packed_floats.argtypes = []
+    L.quad_policy_packed_floats.restype = i32
+    L.quad_policy_pack.argtypes = [C.POINTER(QuadPolicyParams), vp, vp]
+    L.quad_policy_act.argtypes = [vp, C.POINTER(QuadPolicyAct), i32, vp]
+    L.quad_rollout_post.argtypes = [vp, C.POINTER(QuadRolloutPost), i32, vp]
     for n in ("quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
-              "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae"):
+              "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
+              "quad_policy_pack", "quad_policy_act", "quad_rollout_post"):
         getattr(L, n).restype = C.c_int
 
 

@@ -37,6 +37,18 @@ constexpr int BLOCK = 256;
 
 thread_local std::string g_err;
 
+}  // namespace
+
+namespace quadenv {
+// shared with policy.hip: one last-error slot per thread for the whole library
+int set_error(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+}  // namespace quadenv
+
+namespace {
+
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;

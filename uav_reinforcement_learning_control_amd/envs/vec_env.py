@@ -132,7 +132,8 @@ class QuadVecEnv:
         actions: float32 [N,4] on the env's device (not clipped by the env, like HoverEnv).
         The returned tensors are the env's own buffers (overwritten by the next step) unless
         obs/reward are given. info="basic": terminal_observation + TimeLimit.truncated;
-        info="full": also motor_commands, voltage_scale, state (HoverEnv's info dict).
+        info="full": also motor_commands, voltage_scale, state (HoverEnv's info dict);
+        info="raw": terminal_observation only (no extra device op; for graph-captured loops).
         """
         self._check(actions, (self.num_envs, 4), torch.float32)
         obs = self.obs if obs is None else obs
@@ -149,8 +150,9 @@ class QuadVecEnv:
             state12=self.state12.data_ptr() if full else None)
         N.check(N.lib().quad_step(self._h, C.c_void_p(actions.data_ptr()), C.byref(o),
                                   self._stream()), "quad_step")
-        inf = {"terminal_observation": self.terminal_obs,
-               "TimeLimit.truncated": self.truncated & ~self.terminated}
+        inf = {"terminal_observation": self.terminal_obs}
+        if info != "raw":
+            inf["TimeLimit.truncated"] = self.truncated & ~self.terminated
         if full:
             inf.update(motor_commands=self.motor_commands, voltage_scale=self.voltage_scale,
                        state=self.state12)

@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from .fused import FusedPolicy
 from .gae import gae
 from .policy import ActorCritic
 
@@ -48,6 +49,7 @@ class PPOConfig:
     normalize_advantage: bool = True
     net_arch: tuple = (128, 128)
     adam_eps: float = 1e-5
+    fused_policy: bool = True             # rollout policy on the MFMA kernels (ppo/fused.py)
 
 
 def ppo_loss(policy: ActorCritic, obs, act, logp_old, adv, ret, cfg: PPOConfig):
@@ -130,6 +132,10 @@ class PPO:
         self._act_env = torch.zeros(n, 4, **f32)
         self._done_stats = torch.zeros(3, dtype=torch.float64, device=self.device)
         self._graph = None
+        # fused path: running step counter (buffer row = t % n_steps; keys the action noise)
+        self._fp = FusedPolicy(self.policy) if self.cfg.fused_policy else None
+        self._tc = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._noise_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5851F42D4C957F2D) & (2**64 - 1)
 
     # ------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -164,22 +170,40 @@ class PPO:
         self.last_start.copy_(done)
         self._t += 1
 
+    def _rollout_step_fused(self):
+        """The same step as three launches: MFMA policy, env, epilogue (graph-capturable)."""
+        env, T = self.env, self.cfg.n_steps
+        self._fp.act(self.last_obs, self._act_env, actions=self.buf_act, log_prob=self.buf_logp,
+                     value=self.buf_val, obs_copy=self.buf_obs, last_start=self.last_start,
+                     episode_starts=self.buf_start, t_index=self._tc, rows=T,
+                     seed=self._noise_seed, env_id_base=env.env_id_base)
+        _, rew, term, trunc, info = env.step(self._act_env, obs=self.last_obs, info="raw")
+        self._fp.post(rew, term, trunc, info["terminal_observation"], self.buf_rew, self.last_start,
+                      self.ep_ret, self.ep_len, self._done_stats, self._tc, T, self.cfg.gamma)
+
+    def _step_fn(self):
+        return self._rollout_step_fused if self._fp is not None else self._rollout_step
+
     def _capture(self):
         # warm the kernels (rocBLAS handles, allocator) on a side stream, then capture one step
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
+        step = self._step_fn()
         with torch.cuda.stream(s):
-            self._rollout_step()
+            step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._t.zero_()
+        self._tc.zero_()
         self._graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._graph):
-            self._rollout_step()
+            step()
         torch.cuda.synchronize(self.device)
 
     @torch.no_grad()
     def collect_rollouts(self, use_graph: bool = True) -> RolloutStats:
         env, cfg, pol = self.env, self.cfg, self.policy
+        if self._fp is not None:
+            self._fp.pack()  # the kernels' copy of the weights the last update produced
         if not self._started:
             self.last_obs.copy_(env.reset())
             self.last_start.fill_(1.0)
@@ -189,11 +213,12 @@ class PPO:
         t0 = time.perf_counter()
         self._t.zero_()
         self._done_stats.zero_()
+        step = self._step_fn()
         for _ in range(cfg.n_steps):
             if use_graph and self._graph is not None:
                 self._graph.replay()
             else:
-                self._rollout_step()
+                step()
         last_v = pol.value(self.last_obs)
         gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
             cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
