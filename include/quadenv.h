@@ -171,47 +171,56 @@ int32_t quad_policy_packed_floats(void);
  * optimizer update that precedes a rollout; stream-ordered). `packed`: device, 16-byte aligned. */
 int quad_policy_pack(const QuadPolicyParams* p, float* packed, void* stream);
 
-/* One rollout-step policy evaluation (SB3 OnPolicyAlgorithm.collect_rollouts body):
- * a = mean(obs) + exp(log_std) * z, z ~ N(0,1) from Philox(seed; env id, t, 0x200) + Box-Muller;
- * actions_env = clip(a, -1, 1). t = *t_index (0 if NULL) is a running step counter (it is never
- * reset, so successive rollouts draw fresh noise); row outputs go to row t % rows of time-major
- * [rows,N,...] buffers; every row pointer may be NULL. */
-typedef struct QuadPolicyAct {
-  const float* obs;         /* [N,12] */
-  float* actions_env;       /* [N,4] clipped action for quad_step (16-byte aligned) */
-  float* actions;           /* [T,N,4] unclipped sample (rollout buffer) or NULL */
-  float* log_prob;          /* [T,N] or NULL */
-  float* value;             /* [T,N] critic V(obs) or NULL */
-  float* obs_copy;          /* [T,N,12] or NULL */
-  const float* last_start;  /* [N] episode_starts of this step or NULL */
-  float* episode_starts;    /* [T,N] or NULL */
-  const uint32_t* t_index;  /* device step counter or NULL */
-  int32_t rows;             /* T of the [T,N,...] buffers (>= 1) */
-  int32_t deterministic;    /* 1: a = mean (policy.predict(deterministic=True)) */
-  uint64_t seed;
-  uint64_t env_id_base;     /* global id of env 0 (keys the noise per env, shard-independent) */
-} QuadPolicyAct;
-int quad_policy_act(const float* packed, const QuadPolicyAct* a, int32_t n, void* stream);
-
-/* Rollout epilogue after quad_step for row t % rows, t = *t_index, then *t_index += 1:
- * buf_rew[t] = reward + gamma * V(terminal_obs) where truncated && !terminated (TimeLimit
- * bootstrap; the critic runs only on tiles that hold such an env); last_start = done;
- * Monitor statistics: stats[0..2] += (sum of finished returns, lengths, count). */
+/* Rollout epilogue of one step (after quad_step), SB3 collect_rollouts semantics:
+ * buf_rew[row] = reward + gamma * V(terminal_obs) where truncated && !terminated (TimeLimit
+ * bootstrap; the critic runs only on 32-env tiles that hold such an env), else reward;
+ * last_start = terminated | truncated; Monitor statistics: ep_ret/ep_len accumulate and reset on
+ * done, stats[slot] += (finished return, length, 1) -- sum the QUAD_POLICY_STAT_SLOTS slots. */
+enum { QUAD_POLICY_STAT_SLOTS = 1024 };
 typedef struct QuadRolloutPost {
   const float* reward;          /* [N] */
   const uint8_t* terminated;    /* [N] */
   const uint8_t* truncated;     /* [N] */
   const float* terminal_obs;    /* [N,12] */
-  float* buf_rew;               /* [T,N] */
+  float* buf_rew;               /* [rows,N] */
   float* last_start;            /* [N] */
   float* ep_ret;                /* [N] running episode return */
   float* ep_len;                /* [N] running episode length */
-  double* stats;                /* [3] */
-  uint32_t* t_index;            /* device step counter */
-  int32_t rows;                 /* T of buf_rew */
+  double* stats;                /* [QUAD_POLICY_STAT_SLOTS][3], zeroed by the caller */
+  int32_t rows;
   float gamma;
 } QuadRolloutPost;
-int quad_rollout_post(const float* packed, const QuadRolloutPost* p, int32_t n, void* stream);
+
+/* One rollout-step policy evaluation (SB3 OnPolicyAlgorithm.collect_rollouts body):
+ * a = mean(obs) + exp(log_std) * z, z ~ N(0,1) from Philox(seed; env id, t, 0x200) + Box-Muller;
+ * actions_env = clip(a, -1, 1). `cursor` (device uint32[4] = {t, pending, 0, 0}, zero it to start)
+ * holds the running step counter t (never reset, so successive rollouts draw fresh noise); row
+ * outputs go to row t % rows of time-major [rows,N,...] buffers; every row pointer may be NULL.
+ * With `epilogue` != NULL the launch first finishes step t-1 if it is pending (QuadRolloutPost
+ * above, row (t-1) % rows, before episode_starts[t] is taken from last_start), then advances the
+ * cursor to t+1 and marks step t pending: one launch per step besides quad_step. */
+typedef struct QuadPolicyAct {
+  const float* obs;         /* [N,12] */
+  float* actions_env;       /* [N,4] clipped action for quad_step (16-byte aligned) */
+  float* actions;           /* [rows,N,4] unclipped sample (rollout buffer) or NULL */
+  float* log_prob;          /* [rows,N] or NULL */
+  float* value;             /* [rows,N] critic V(obs) or NULL */
+  float* obs_copy;          /* [rows,N,12] or NULL */
+  const float* last_start;  /* [N] episode_starts of this step or NULL */
+  float* episode_starts;    /* [rows,N] or NULL */
+  uint32_t* cursor;         /* device uint32[4] or NULL (t = 0, read-only without epilogue) */
+  int32_t rows;             /* >= 1 */
+  int32_t deterministic;    /* 1: a = mean (policy.predict(deterministic=True)) */
+  uint64_t seed;
+  uint64_t env_id_base;     /* global id of env 0 (keys the noise per env, shard-independent) */
+  const QuadRolloutPost* epilogue;  /* fused epilogue of step t-1, or NULL */
+} QuadPolicyAct;
+int quad_policy_act(const float* packed, const QuadPolicyAct* a, int32_t n, void* stream);
+
+/* Finish the pending step (end of a rollout): the epilogue for row (t-1) % rows if the cursor
+ * marks one pending, then clears the mark. A no-op otherwise. */
+int quad_rollout_post(const float* packed, const QuadRolloutPost* p, uint32_t* cursor, int32_t n,
+                      void* stream);
 
 #ifdef __cplusplus
 }

@@ -121,8 +121,9 @@ def test_sampled_actions_logp_and_rows():
                episode_starts=torch.full((T, n), 7.0, device="cuda"))
     last_start = (torch.arange(n, device="cuda") % 3 == 0).float()
     t = 7  # row 7 % 5 = 2
-    tix = torch.tensor([t], dtype=torch.int32, device="cuda")
-    fp.act(obs, act_env, last_start=last_start, t_index=tix, rows=T, seed=seed, env_id_base=base, **buf)
+    cur = torch.tensor([t, 0, 0, 0], dtype=torch.int32, device="cuda")
+    fp.act(obs, act_env, last_start=last_start, cursor=cur, rows=T, seed=seed, env_id_base=base, **buf)
+    assert cur.tolist() == [t, 0, 0, 0]  # read-only without an epilogue
     row = t % T
     for k, b in buf.items():  # other rows untouched
         others = torch.cat([b[:row], b[row + 1:]])
@@ -151,11 +152,7 @@ def test_sampled_actions_logp_and_rows():
     assert abs((z2 ** 4).mean().item() - 3) < 0.1
 
 
-def test_rollout_post_bootstrap_stats_and_counter():
-    pol = _policy(4)
-    fp = _fused(pol)
-    n, T, gamma = 5000, 4, 0.99
-    g = torch.Generator(device="cuda").manual_seed(5)
+def _epi_case(n, g):
     rew = torch.rand(n, device="cuda", generator=g)
     term = torch.rand(n, device="cuda", generator=g) < 0.05
     trunc = torch.zeros(n, dtype=torch.bool, device="cuda")
@@ -163,30 +160,73 @@ def test_rollout_post_bootstrap_stats_and_counter():
     trunc[4990] = True
     term[1010] = True                # terminated and truncated: no bootstrap
     tobs = torch.rand(n, 12, device="cuda", generator=g) * 2 - 1
+    return rew, term, trunc, tobs
+
+
+@pytest.mark.parametrize("fused", [True, False], ids=["in_act", "post"])
+def test_epilogue_bootstrap_stats_and_cursor(fused):
+    from uav_reinforcement_learning_control_amd import _native as N
+    pol = _policy(4)
+    fp = _fused(pol)
+    n, T, gamma = 5000, 4, 0.99
+    g = torch.Generator(device="cuda").manual_seed(5)
+    rew, term, trunc, tobs = _epi_case(n, g)
     buf_rew = torch.full((T, n), -5.0, device="cuda")
     last_start = torch.full((n,), 9.0, device="cuda")
     ep_ret = torch.rand(n, device="cuda", generator=g) * 10
     ep_len = torch.randint(0, 100, (n,), device="cuda", generator=g).float()
-    stats = torch.zeros(3, dtype=torch.float64, device="cuda")
-    tix = torch.tensor([6], dtype=torch.int32, device="cuda")
+    slots = torch.zeros(N.POLICY_STAT_SLOTS, 3, dtype=torch.float64, device="cuda")
+    cur = torch.tensor([7, 1, 0, 0], dtype=torch.int32, device="cuda")  # step 6 pending
     ret0, len0 = ep_ret.clone(), ep_len.clone()
-    fp.post(rew, term, trunc, tobs, buf_rew, last_start, ep_ret, ep_len, stats, tix, T, gamma)
+    epi = fp.make_epilogue(rew, term, trunc, tobs, buf_rew, last_start, ep_ret, ep_len, slots, T, gamma)
+    obs = torch.rand(n, 12, device="cuda") * 2 - 1
+    starts = torch.full((T, n), -1.0, device="cuda")
+    if fused:
+        fp.act(obs, torch.empty(n, 4, device="cuda"), last_start=last_start, episode_starts=starts,
+               cursor=cur, rows=T, epilogue=epi)
+        assert cur.tolist() == [8, 1, 0, 0]
+    else:
+        fp.post(epi, cur)
+        assert cur.tolist() == [7, 0, 0, 0]
+        fp.post(epi, cur)  # nothing pending: a no-op
     torch.cuda.synchronize()
-    assert tix.item() == 7
     timeout = trunc & ~term
     done = term | trunc
     with torch.no_grad():
         tv = pol.value(tobs)
     want = torch.where(timeout, rew + gamma * tv, rew)
-    _close(buf_rew[2].cpu(), want.cpu())
+    _close(buf_rew[2].cpu(), want.cpu())   # row (7 - 1) % 4
     assert torch.all(torch.cat([buf_rew[:2], buf_rew[3:]]) == -5.0)
     assert torch.equal(last_start, done.float())
+    if fused:  # episode_starts of step 7 (row 3) is the epilogue's last_start
+        assert torch.equal(starts[3], done.float())
     assert torch.equal(ep_ret, torch.where(done, 0.0, ret0 + rew))
     assert torch.equal(ep_len, torch.where(done, 0.0, len0 + 1))
     fr, fl = (ret0 + rew)[done].double(), (len0 + 1)[done].double()
-    s = stats.cpu().numpy()
+    s = slots.sum(0).cpu().numpy()
     assert s[2] == done.sum().item() and s[1] == fl.sum().item()
     assert abs(s[0] - fr.sum().item()) <= 1e-4 * (1 + abs(fr.sum().item()))
+
+
+def test_cursor_advances_over_many_launches():
+    """The last-block cursor update is grid-wide: 50 launches at a size with several tiles per
+    wave advance t by exactly 50 and keep the pending mark."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    pol = _policy(6)
+    fp = _fused(pol)
+    n, T = 200_000, 3
+    f = lambda *s: torch.zeros(*s, device="cuda")
+    rew, buf_rew, ls, er, el = f(n), f(T, n), f(n), f(n), f(n)
+    tb = torch.zeros(n, dtype=torch.bool, device="cuda")
+    slots = torch.zeros(N.POLICY_STAT_SLOTS, 3, dtype=torch.float64, device="cuda")
+    epi = fp.make_epilogue(rew, tb, tb, f(n, 12), buf_rew, ls, er, el, slots, T, 0.9)
+    cur = torch.zeros(4, dtype=torch.int32, device="cuda")
+    obs, ae = f(n, 12), f(n, 4)
+    for _ in range(50):
+        fp.act(obs, ae, cursor=cur, rows=T, epilogue=epi)
+    torch.cuda.synchronize()
+    assert cur.tolist() == [50, 1, 0, 0]
+    assert torch.all(el == 49.0)  # 49 epilogues ran (the first launch had nothing pending)
 
 
 def test_policy_rejects_bad_arguments():

@@ -34,7 +34,7 @@ def test_graph_rollout_buffers_are_consistent(fused):
     # an episode start follows every done: starts are 0/1 and many episodes ended (random policy)
     st = m.buf_start.cpu().numpy()
     assert set(np.unique(st)) <= {0.0, 1.0} and rs.episodes > 0
-    assert (m._tc.item() == 48) if fused else (m._t.item() == 24)
+    assert (m._cursor[0].item() == 48 and m._cursor[1].item() == 0) if fused else (m._t.item() == 24)
     # the obs rows chain: obs[t+1] of an env that did not finish is the env's next obs
     assert torch.isfinite(m.buf_obs).all() and torch.all(m.buf_obs.abs() <= 1.0 + 1e-6)
 
@@ -43,7 +43,7 @@ def test_graph_rollout_buffers_are_consistent(fused):
 def test_eager_and_graph_rollouts_agree_on_semantics(fused):
     m = _ppo(1024, 8, n_epochs=1, n_minibatches=2, fused_policy=fused)
     m.collect_rollouts(use_graph=False)
-    assert ((m._tc.item() == 8) if fused else (m._t.item() == 8)) and torch.isfinite(m.buf_ret).all()
+    assert ((m._cursor[0].item() == 8) if fused else (m._t.item() == 8)) and torch.isfinite(m.buf_ret).all()
 
 
 def test_fused_rollout_matches_replayed_env():

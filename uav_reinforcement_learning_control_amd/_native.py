@@ -56,19 +56,23 @@ class QuadPolicyParams(C.Structure):
                                           "log_std")]
 
 
-class QuadPolicyAct(C.Structure):
-    _fields_ = [("obs", C.c_void_p), ("actions_env", C.c_void_p), ("actions", C.c_void_p),
-                ("log_prob", C.c_void_p), ("value", C.c_void_p), ("obs_copy", C.c_void_p),
-                ("last_start", C.c_void_p), ("episode_starts", C.c_void_p),
-                ("t_index", C.c_void_p), ("rows", C.c_int32), ("deterministic", C.c_int32),
-                ("seed", C.c_uint64), ("env_id_base", C.c_uint64)]
+POLICY_STAT_SLOTS = 1024
 
 
 class QuadRolloutPost(C.Structure):
     _fields_ = [("reward", C.c_void_p), ("terminated", C.c_void_p), ("truncated", C.c_void_p),
                 ("terminal_obs", C.c_void_p), ("buf_rew", C.c_void_p), ("last_start", C.c_void_p),
                 ("ep_ret", C.c_void_p), ("ep_len", C.c_void_p), ("stats", C.c_void_p),
-                ("t_index", C.c_void_p), ("rows", C.c_int32), ("gamma", C.c_float)]
+                ("rows", C.c_int32), ("gamma", C.c_float)]
+
+
+class QuadPolicyAct(C.Structure):
+    _fields_ = [("obs", C.c_void_p), ("actions_env", C.c_void_p), ("actions", C.c_void_p),
+                ("log_prob", C.c_void_p), ("value", C.c_void_p), ("obs_copy", C.c_void_p),
+                ("last_start", C.c_void_p), ("episode_starts", C.c_void_p),
+                ("cursor", C.c_void_p), ("rows", C.c_int32), ("deterministic", C.c_int32),
+                ("seed", C.c_uint64), ("env_id_base", C.c_uint64),
+                ("epilogue", C.POINTER(QuadRolloutPost))]
 
 
 # every symbol include/quadenv.h declares (checked by tests/test_abi.py)
@@ -108,7 +112,7 @@ def _declare(L):
     L.quad_policy_packed_floats.restype = i32
     L.quad_policy_pack.argtypes = [C.POINTER(QuadPolicyParams), vp, vp]
     L.quad_policy_act.argtypes = [vp, C.POINTER(QuadPolicyAct), i32, vp]
-    L.quad_rollout_post.argtypes = [vp, C.POINTER(QuadRolloutPost), i32, vp]
+    L.quad_rollout_post.argtypes = [vp, C.POINTER(QuadRolloutPost), vp, i32, vp]
     for n in ("quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
               "quad_policy_pack", "quad_policy_act", "quad_rollout_post"):

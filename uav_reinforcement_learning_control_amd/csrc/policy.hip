@@ -1,6 +1,6 @@
 // policy.hip -- the PPO rollout policy (SB3 ActorCritic as configured by train.py:50-68:
 // separate actor / critic MLPs 12 -> 128 -> 128, ReLU, action head 4, value head 1, fp32) as
-// MFMA kernels for gfx950, plus the per-step rollout epilogue.
+// MFMA kernels for gfx950, with the per-step rollout epilogue fused in.
 //
 // Layout trick: every hidden layer is computed TRANSPOSED, H^T = W . X^T, with
 // v_mfma_f32_32x32x2_f32 (A = weights, B = activations). A 32x32 accumulator tile then holds
@@ -8,9 +8,14 @@
 // 4 (lane >> 5)), which is exactly the B-operand layout of the next layer if k-step r of that layer
 // consumes the input neurons held in register r -- so the whole MLP stays in registers. The
 // weights are packed once per rollout (k_policy_pack) into that permuted fragment order and staged
-// in LDS (148 KB for actor + critic). Output heads (4 and 1 wide) run on the VALU with one
-// lane-half exchange. f32-input MFMA is exact f32 (an ordered fma chain), the VALU-rate
-// peak, and one wave per SIMD already saturates the matrix pipe.
+// in LDS (152 KB for actor + critic; one 4-wave block per CU, grid-stride over 32-env tiles).
+// Output heads (4 and 1 wide) run on the VALU with one lane-half exchange. f32-input MFMA is exact
+// f32 (an ordered fma chain) at the VALU-rate peak; one wave per SIMD saturates the matrix pipe.
+//
+// Rollout step t = one k_policy_act launch + one quad_step launch. k_policy_act first finishes
+// step t-1 (reward row with the TimeLimit bootstrap, episode_starts, Monitor statistics) when the
+// cursor says it is pending, then evaluates the policy for step t; its last block to finish
+// advances the cursor. quad_rollout_post finishes the final step of a rollout.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -29,24 +34,29 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 namespace {
 
 constexpr int H = 128, OBS = 12, ACT = 4;
-constexpr int TILE = 32;          // envs per MFMA tile (one wave holds one tile at a time)
-constexpr int PBLOCK = 256;       // 4 waves
+constexpr int TILE = 32;     // envs per MFMA tile (one wave holds one tile at a time)
+constexpr int PBLOCK = 256;  // 4 waves
+constexpr int NT_ACT = 2;    // tiles per wave iteration in k_policy_act (shared weight fragments)
 
-// packed net image (floats), identical layout for actor and critic:
-//   W1: [4 n][6 s][64 lane]            A fragments of layer 1 (K = 12 -> 6 k-steps of 2)
-//   W2: [4 m][4 n][4 q][64 lane][4 r]   A fragments of layer 2, k-step r + 4q of input tile n
-//   B1, B2: [4 tile][16 reg][2 half]    biases in accumulator order
-//   W3: [4 out][4 tile][16 reg][2 half] head weights in accumulator order (critic: 1 out)
+// packed net image (floats); NOUT = 4 (actor) or 1 (critic):
+//   W1: [4 n][64 lane][8]              layer-1 A fragments, k-steps s = 0..5 (6, 7 zero)
+//   W2: [4 m][4 n][4 q][64 lane][4 r]   layer-2 A fragments, k-step 4q + r of input tile n
+//   B1, B2: [4 tile][2 half][16 reg]    biases in accumulator order
+//   W3 actor:  [4 m][16 reg][2 half][4 out]   head weights in accumulator order
+//   W3 critic: [4 m][4 rq][2 half][4 r]       (reg = 4 rq + r)
 //   B3: [4]
-constexpr int W1_F = 4 * 6 * 64, W2_F = 4 * 4 * 4 * 64 * 4, B_F = 4 * 16 * 2;
+constexpr int W1_F = 4 * 64 * 8, W2_F = 4 * 4 * 4 * 64 * 4, B_F = 4 * 2 * 16;
 constexpr int NET_W1 = 0, NET_W2 = NET_W1 + W1_F, NET_B1 = NET_W2 + W2_F, NET_B2 = NET_B1 + B_F;
 constexpr int NET_W3 = NET_B2 + B_F;
-constexpr int ACTOR_F = NET_W3 + ACT * B_F + 4;
-constexpr int CRITIC_F = NET_W3 + 1 * B_F + 4;
-constexpr int PACKED_F = ACTOR_F + CRITIC_F + 4;  // + log_std[4]
-constexpr int LDS_F = ACTOR_F + CRITIC_F;         // 37,224 floats = 148.9 KB
+constexpr int ACTOR_F = NET_W3 + ACT * 128 + 4;
+constexpr int CRITIC_F = NET_W3 + 128 + 4;
+constexpr int LDS_F = ACTOR_F + CRITIC_F;  // 38,024 floats = 152 KB
+constexpr int PACKED_F = LDS_F + 4;        // + log_std[4]
+static_assert(ACTOR_F % 4 == 0 && LDS_F % 4 == 0, "float4 staging");
 
-__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+enum { CUR_T = 0, CUR_PENDING = 1, CUR_ARRIVED = 2 };
+
+__host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 // ---- pack: one thread per packed float
 struct NetPtrs {
@@ -54,32 +64,35 @@ struct NetPtrs {
 };
 
 __device__ float pack_one(const NetPtrs& p, int nout, int idx) {
-  if (idx < NET_W2) {  // W1[n][s][lane]: A[i = lane&31][k = lane>>5] of tile n, k-step s
-    const int lane = idx % 64, s = (idx / 64) % 6, n = idx / 384;
-    return p.w0[(32 * n + (lane & 31)) * OBS + 2 * s + (lane >> 5)];
+  if (idx < NET_W2) {  // A[i = lane&31][k = lane>>5] of tile n, k-step s
+    const int s = idx % 8, lane = (idx / 8) % 64, n = idx / 512;
+    return s < 6 ? p.w0[(32 * n + (lane & 31)) * OBS + 2 * s + (lane >> 5)] : 0.f;
   }
-  if (idx < NET_B1) {  // W2[m][n][q][lane][r]
+  if (idx < NET_B1) {
     int t = idx - NET_W2;
     const int r = t % 4; t /= 4;
     const int lane = t % 64; t /= 64;
     const int q = t % 4; t /= 4;
     const int n = t % 4, m = t / 4;
-    const int kreg = 4 * q + r;  // register of the input tile consumed at this k-step
-    const int in = 32 * n + acc_row(kreg, lane >> 5);
+    const int in = 32 * n + acc_row(4 * q + r, lane >> 5);  // input neuron held in register 4q+r
     return p.w1[(32 * m + (lane & 31)) * H + in];
   }
-  if (idx < NET_W3) {  // B1 / B2 [tile][reg][half]
+  if (idx < NET_W3) {
     const bool second = idx >= NET_B2;
     const int t = idx - (second ? NET_B2 : NET_B1);
-    const int h = t % 2, r = (t / 2) % 16, tile = t / 32;
+    const int r = t % 16, h = (t / 16) % 2, tile = t / 32;
     return (second ? p.b1 : p.b0)[32 * tile + acc_row(r, h)];
   }
   int t = idx - NET_W3;
-  if (t < nout * B_F) {  // W3[out][tile][reg][half]
-    const int h = t % 2, r = (t / 2) % 16, tile = (t / 32) % 4, o = t / 128;
-    return p.w2[o * H + 32 * tile + acc_row(r, h)];
+  if (t < nout * 128) {
+    if (nout == ACT) {
+      const int o = t % 4, h = (t / 4) % 2, r = (t / 8) % 16, m = t / 128;
+      return p.w2[o * H + 32 * m + acc_row(r, h)];
+    }
+    const int r4 = t % 4, h = (t / 4) % 2, rq = (t / 8) % 4, m = t / 32;
+    return p.w2[32 * m + acc_row(4 * rq + r4, h)];
   }
-  t -= nout * B_F;
+  t -= nout * 128;
   return t < nout ? p.b2[t] : 0.f;
 }
 
@@ -89,75 +102,141 @@ __global__ void k_policy_pack(NetPtrs actor, NetPtrs critic, const float* __rest
   if (idx >= PACKED_F) return;
   float v;
   if (idx < ACTOR_F) v = pack_one(actor, ACT, idx);
-  else if (idx < ACTOR_F + CRITIC_F) v = pack_one(critic, 1, idx - ACTOR_F);
-  else v = log_std[idx - ACTOR_F - CRITIC_F];
+  else if (idx < LDS_F) v = pack_one(critic, 1, idx - ACTOR_F);
+  else v = log_std[idx - LDS_F];
   out[idx] = v;
 }
 
-// ---- the MLP trunk of one net for one 32-env tile: returns head outputs (per env, combined over
-// the two lane halves), NOUT of them. X^T fragments: xb[s] = obs[env = lane&31][2 s + (lane>>5)].
-template <int NOUT>
-__device__ __forceinline__ void net_forward(const float* __restrict__ L, const float xb[6], float out[NOUT]) {
+__device__ __forceinline__ float4 ld4(const float* L, int off) {
+  return *reinterpret_cast<const float4*>(L + off);
+}
+
+__device__ __forceinline__ void bias_init(f32x16& acc, const float* L, int off) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const float4 b = ld4(L, off + 4 * j);
+    acc[4 * j] = b.x; acc[4 * j + 1] = b.y; acc[4 * j + 2] = b.z; acc[4 * j + 3] = b.w;
+  }
+}
+
+// ---- one net's forward for NT 32-env tiles at once (all 64 lanes). X^T fragments:
+// xb[j][s] = x[env = lane&31 of tile j][2 s + (lane>>5)]. Returns the NOUT head outputs of env
+// lane&31 of every tile (both lane halves get them). The NT tiles share every LDS weight fragment,
+// and their MFMA chains interleave, so consecutive MFMAs are independent.
+template <int NOUT, int NT>
+__device__ __forceinline__ void net_forward(const float* __restrict__ L, const float (&xb)[NT][6],
+                                            float (&out)[NT][NOUT]) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
-  f32x16 h1[4];
+  f32x16 h1[NT][4];
 #pragma unroll
   for (int n = 0; n < 4; n++) {
-    f32x16 acc;
+    f32x16 b;
+    bias_init(b, L, NET_B1 + (n * 2 + h) * 16);
+    const float4 wa = ld4(L, NET_W1 + (n * 64 + lane) * 8), wb = ld4(L, NET_W1 + (n * 64 + lane) * 8 + 4);
+    const float w[6] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y};
+    f32x16 acc[NT];
 #pragma unroll
-    for (int r = 0; r < 16; r++) acc[r] = L[NET_B1 + (n * 16 + r) * 2 + h];
+    for (int j = 0; j < NT; j++) acc[j] = b;
 #pragma unroll
     for (int s = 0; s < 6; s++)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(L[NET_W1 + (n * 6 + s) * 64 + lane], xb[s], acc, 0, 0, 0);
 #pragma unroll
-    for (int r = 0; r < 16; r++) acc[r] = fmaxf(acc[r], 0.f);  // ReLU
-    h1[n] = acc;
+      for (int j = 0; j < NT; j++) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[s], xb[j][s], acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[j][r] = fmaxf(acc[j][r], 0.f);  // ReLU
+      h1[j][n] = acc[j];
+    }
   }
-  float part[NOUT];
+  float part[NT][NOUT];
 #pragma unroll
-  for (int o = 0; o < NOUT; o++) part[o] = 0.f;
+  for (int j = 0; j < NT; j++)
+#pragma unroll
+    for (int o = 0; o < NOUT; o++) part[j][o] = 0.f;
 #pragma unroll 1
   for (int m = 0; m < 4; m++) {
-    f32x16 acc;
+    f32x16 acc[NT];
+    bias_init(acc[0], L, NET_B2 + (m * 2 + h) * 16);
 #pragma unroll
-    for (int r = 0; r < 16; r++) acc[r] = L[NET_B2 + (m * 16 + r) * 2 + h];
+    for (int j = 1; j < NT; j++) acc[j] = acc[0];
 #pragma unroll
     for (int n = 0; n < 4; n++) {
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        const float4 a4 = *reinterpret_cast<const float4*>(&L[NET_W2 + (((m * 4 + n) * 4 + q) * 64 + lane) * 4]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, h1[n][4 * q + 0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, h1[n][4 * q + 1], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, h1[n][4 * q + 2], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, h1[n][4 * q + 3], acc, 0, 0, 0);
+        const float4 a4 = ld4(L, NET_W2 + (((m * 4 + n) * 4 + q) * 64 + lane) * 4);
+        const float w[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+#pragma unroll
+          for (int j = 0; j < NT; j++)
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[k], h1[j][n][4 * q + k], acc[j], 0, 0, 0);
       }
     }
     // ReLU, then this 32-neuron slice's contribution to the head (VALU)
+    if constexpr (NOUT == ACT) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) {
-      const float a = fmaxf(acc[r], 0.f);
+      for (int r = 0; r < 16; r++) {
+        const float4 w = ld4(L, NET_W3 + ((m * 16 + r) * 2 + h) * 4);
 #pragma unroll
-      for (int o = 0; o < NOUT; o++) part[o] = fmaf(L[NET_W3 + ((o * 4 + m) * 16 + r) * 2 + h], a, part[o]);
+        for (int j = 0; j < NT; j++) {
+          const float x = fmaxf(acc[j][r], 0.f);
+          part[j][0] = fmaf(w.x, x, part[j][0]);
+          part[j][1] = fmaf(w.y, x, part[j][1]);
+          part[j][2] = fmaf(w.z, x, part[j][2]);
+          part[j][3] = fmaf(w.w, x, part[j][3]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int rq = 0; rq < 4; rq++) {
+        const float4 w = ld4(L, NET_W3 + ((m * 4 + rq) * 2 + h) * 4);
+#pragma unroll
+        for (int j = 0; j < NT; j++) {
+          part[j][0] = fmaf(w.x, fmaxf(acc[j][4 * rq + 0], 0.f), part[j][0]);
+          part[j][0] = fmaf(w.y, fmaxf(acc[j][4 * rq + 1], 0.f), part[j][0]);
+          part[j][0] = fmaf(w.z, fmaxf(acc[j][4 * rq + 2], 0.f), part[j][0]);
+          part[j][0] = fmaf(w.w, fmaxf(acc[j][4 * rq + 3], 0.f), part[j][0]);
+        }
+      }
     }
   }
-  // lanes l and l ^ 32 hold the two halves of the same env's neurons
+  // lanes l and l ^ 32 hold the two halves of the same env's neurons; both lanes form the same sum
 #pragma unroll
-  for (int o = 0; o < NOUT; o++) {
-    const float other = __shfl_xor(part[o], 32);
-    out[o] = (part[o] + other) + L[NET_W3 + NOUT * B_F + o];
-  }
+  for (int j = 0; j < NT; j++)
+#pragma unroll
+    for (int o = 0; o < NOUT; o++) {
+      const float other = __shfl_xor(part[j][o], 32);
+      out[j][o] = ((h ? other : part[j][o]) + (h ? part[j][o] : other)) + L[NET_W3 + NOUT * 128 + o];
+    }
 }
 
+// 152 KB global -> LDS per block: batches of 13 float4 loads in flight per thread (a serial
+// load -> store loop would pay ~38 round trips of L2/MALL latency)
 __device__ __forceinline__ void stage_lds(float* lds, const float* __restrict__ packed) {
+  constexpr int NV = LDS_F / 4, PER = (NV + PBLOCK - 1) / PBLOCK, BATCH = 13;
   const float4* src = reinterpret_cast<const float4*>(packed);
   float4* dst = reinterpret_cast<float4*>(lds);
-  for (int k = threadIdx.x; k < LDS_F / 4; k += PBLOCK) dst[k] = src[k];
+#pragma unroll
+  for (int b0 = 0; b0 < PER; b0 += BATCH) {
+    float4 v[BATCH];
+#pragma unroll
+    for (int j = 0; j < BATCH; j++) {
+      const int k = (b0 + j) * PBLOCK + threadIdx.x;
+      v[j] = src[k < NV ? k : NV - 1];  // clamped: every element defined, stays in VGPRs
+    }
+#pragma unroll
+    for (int j = 0; j < BATCH; j++) {
+      const int k = (b0 + j) * PBLOCK + threadIdx.x;
+      if (b0 + j < PER && k < NV) dst[k] = v[j];
+    }
+  }
   __syncthreads();
 }
 
-__device__ __forceinline__ void load_xb(const float* __restrict__ obs, int env, bool ok, float xb[6]) {
+__device__ __forceinline__ void load_xb(const float* __restrict__ x, int env, bool ok, float xb[6]) {
   const int h = (threadIdx.x & 63) >> 5;
 #pragma unroll
-  for (int s = 0; s < 6; s++) xb[s] = ok ? obs[size_t(env) * OBS + 2 * s + h] : 0.f;
+  for (int s = 0; s < 6; s++) xb[s] = ok ? x[size_t(env) * OBS + 2 * s + h] : 0.f;
 }
 
 // Box-Muller on Philox(seed; env, step, 0x200) -> 4 standard normals
@@ -176,146 +255,223 @@ __device__ __forceinline__ void gauss4(uint64_t seed, uint64_t env, uint32_t ste
   }
 }
 
-struct ActArgs {
-  const float* obs;        // [N,12]
-  float* act_env;          // [N,4] clipped
-  float* act;              // [N,4] unclipped sample (buffer row) or NULL
-  float* logp;             // [N] or NULL
-  float* value;            // [N] or NULL
-  float* obs_copy;         // [N,12] or NULL
-  const float* last_start; // [N] or NULL
-  float* starts;           // [T,N] or NULL
-  const uint32_t* t_index; // device step counter (row t % rows of the buffers) or NULL
-  int32_t rows;
-  uint64_t seed;
-  uint64_t env_base;
-  int32_t n;
-  int32_t deterministic;
-};
-
-__global__ __launch_bounds__(PBLOCK) void k_policy_act(const float* __restrict__ packed, ActArgs a) {
-  extern __shared__ float lds[];
-  stage_lds(lds, packed);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
-  const int tiles = (a.n + TILE - 1) / TILE;
-  const uint32_t t = a.t_index ? *a.t_index : 0u;
-  const size_t row0 = size_t(t % uint32_t(a.rows)) * a.n;
-  for (int tile = blockIdx.x * 4 + wave; tile < tiles; tile += gridDim.x * 4) {
-    const int env = tile * TILE + (lane & 31);
-    const bool ok = env < a.n;
-    float xb[6];
-    load_xb(a.obs, env, ok, xb);
-    float mean[ACT], val[1];
-    net_forward<ACT>(lds, xb, mean);
-    net_forward<1>(lds + ACTOR_F, xb, val);
-    if (!ok) continue;
-    if (a.obs_copy) {
-#pragma unroll
-      for (int s = 0; s < 6; s++) a.obs_copy[(row0 + env) * OBS + 2 * s + h] = xb[s];
-    }
-    if (h) continue;  // one lane per env from here
-    if (a.starts) a.starts[row0 + env] = a.last_start ? a.last_start[env] : 0.f;
-    const float* log_std = packed + ACTOR_F + CRITIC_F;
-    float z[ACT] = {0.f, 0.f, 0.f, 0.f};
-    if (!a.deterministic) gauss4(a.seed, a.env_base + uint64_t(env), t, z);
-    float act[ACT], lp = 0.f;
-#pragma unroll
-    for (int j = 0; j < ACT; j++) {
-      const float sd = expf(log_std[j]);
-      act[j] = mean[j] + sd * z[j];
-      const float zz = (act[j] - mean[j]) / sd;  // as PPO.train recomputes it (policy.log_prob)
-      lp += -0.5f * zz * zz - log_std[j] - 0.91893853320467274f;  // 0.5 log(2 pi)
-    }
-    reinterpret_cast<float4*>(a.act_env)[env] =
-        make_float4(fminf(fmaxf(act[0], -1.f), 1.f), fminf(fmaxf(act[1], -1.f), 1.f),
-                    fminf(fmaxf(act[2], -1.f), 1.f), fminf(fmaxf(act[3], -1.f), 1.f));
-    if (a.act) reinterpret_cast<float4*>(a.act + row0 * ACT)[env] = make_float4(act[0], act[1], act[2], act[3]);
-    if (a.logp) a.logp[row0 + env] = lp;
-    if (a.value) a.value[row0 + env] = val[0];
-  }
-}
-
-// Rollout epilogue for step t (after quad_step): TimeLimit bootstrap r += gamma V(terminal_obs)
-// where truncated & !terminated (critic run only on tiles that need it), reward buffer row,
-// episode_start for t + 1, Monitor episode statistics, t += 1.
-struct PostArgs {
+struct EpiArgs {  // QuadRolloutPost, flattened
   const float* reward;
   const uint8_t* terminated;
   const uint8_t* truncated;
   const float* terminal_obs;
-  float* buf_rew;        // [T,N]
-  float* last_start;     // [N] episode_starts for the next step
-  float* ep_ret;         // [N]
-  float* ep_len;         // [N]
-  double* stats;         // [3]: sum of finished returns, lengths, count
-  const uint32_t* t_index;
+  float* buf_rew;
+  float* last_start;
+  float* ep_ret;
+  float* ep_len;
+  double* stats;
   int32_t rows;
   float gamma;
-  int32_t n;
 };
 
-__global__ __launch_bounds__(PBLOCK) void k_rollout_post(const float* __restrict__ packed, PostArgs a) {
-  extern __shared__ float lds[];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int tiles = (a.n + TILE - 1) / TILE;
-  // does any tile of this block need the critic? (stage the weights only then)
-  bool need = false;
-  for (int tile = blockIdx.x * 4; tile < blockIdx.x * 4 + 4 && tile < tiles; tile++) {
-    const int env = tile * TILE + (lane & 31);
-    if (env < a.n) need |= a.truncated[env] && !a.terminated[env];
+// Everything a tile reads from HBM, loaded in one go (issued a tile ahead, see k_policy_act).
+struct TileIn {
+  float xb[6];           // X^T fragments of the obs rows
+  float rew, ret, len;   // epilogue inputs (step t-1)
+  uint32_t flags;        // bit0 terminated, bit1 truncated
+};
+
+__device__ __forceinline__ void load_tile(TileIn& in, const float* __restrict__ obs, const EpiArgs& e,
+                                          bool pend, int env, bool ok) {
+  load_xb(obs, env, ok, in.xb);
+  in.rew = in.ret = in.len = 0.f;
+  in.flags = 0u;
+  if (pend && ok) {
+    in.flags = uint32_t(e.terminated[env] != 0) | (uint32_t(e.truncated[env] != 0) << 1);
+    in.rew = e.reward[env];
+    in.ret = e.ep_ret[env];
+    in.len = e.ep_len[env];
   }
-  need = __syncthreads_or(need);
-  if (need) stage_lds(lds, packed);
-  const size_t row0 = size_t(*a.t_index % uint32_t(a.rows)) * a.n;
-  const int tile = blockIdx.x * 4 + wave;
-  float dret = 0.f, dlen = 0.f, dcnt = 0.f;
-  if (tile < tiles) {
-    const int env = tile * TILE + (lane & 31);
-    const bool ok = env < a.n;
-    const bool timeout = ok && a.truncated[env] && !a.terminated[env];
-    float tv = 0.f;
-    if (__any(timeout)) {
-      float xb[6], v[1];
-      load_xb(a.terminal_obs, env, ok, xb);
-      net_forward<1>(lds + ACTOR_F, xb, v);
-      tv = v[0];
-    }
-    if (ok && (lane >> 5) == 0) {
-      const float r = a.reward[env];
-      a.buf_rew[row0 + env] = timeout ? r + a.gamma * tv : r;
-      const bool done = a.terminated[env] || a.truncated[env];
-      const float ret = a.ep_ret[env] + r, len = a.ep_len[env] + 1.f;
-      if (done) { dret = ret; dlen = len; dcnt = 1.f; }
-      a.ep_ret[env] = done ? 0.f : ret;
-      a.ep_len[env] = done ? 0.f : len;
-      a.last_start[env] = done ? 1.f : 0.f;
-    }
+}
+
+// finish step t-1 for one tile: TimeLimit bootstrap r += gamma V(terminal_obs) where truncated and
+// not terminated (critic only when the tile holds such an env), reward row, last_start, episode
+// statistics (accumulated in st[3] of the h == 0 lanes). Returns the env's new last_start.
+__device__ __forceinline__ float epilogue_tile(const float* __restrict__ Lc, const EpiArgs& e,
+                                               const TileIn& in, int env, bool ok, size_t row, float st[3]) {
+  const int h = (threadIdx.x & 63) >> 5;
+  const bool term = in.flags & 1u, trunc = in.flags & 2u;
+  const bool timeout = ok && trunc && !term;
+  float tv = 0.f;
+  if (__any(timeout)) {
+    float xb[1][6], v[1][1];
+    load_xb(e.terminal_obs, env, ok, xb[0]);
+    net_forward<1, 1>(Lc, xb, v);
+    tv = v[0][0];
   }
-  // block reduction of the episode statistics -> one atomic per block
+  const bool done = term || trunc;
+  if (ok && h == 0) {
+    e.buf_rew[row + env] = timeout ? in.rew + e.gamma * tv : in.rew;
+    const float ret = in.ret + in.rew, len = in.len + 1.f;
+    if (done) { st[0] += ret; st[1] += len; st[2] += 1.f; }
+    e.ep_ret[env] = done ? 0.f : ret;
+    e.ep_len[env] = done ? 0.f : len;
+    e.last_start[env] = done ? 1.f : 0.f;
+  }
+  return done ? 1.f : 0.f;
+}
+
+// block-reduce the episode statistics into this block's slot (uncontended atomics)
+__device__ void flush_stats(double* stats, float st[3]) {
   __shared__ float red[3][PBLOCK / 64];
-  for (int off = 32; off > 0; off >>= 1) {
-    dret += __shfl_down(dret, off);
-    dlen += __shfl_down(dlen, off);
-    dcnt += __shfl_down(dcnt, off);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    float v = st[j];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off);
+    if (lane == 0) red[j][wave] = v;
   }
-  if (lane == 0) { red[0][wave] = dret; red[1][wave] = dlen; red[2][wave] = dcnt; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    float s = 0.f;
+    for (int w = 0; w < PBLOCK / 64; w++) s += red[threadIdx.x][w];
+    if (s != 0.f) atomicAdd(&stats[(blockIdx.x % QUAD_POLICY_STAT_SLOTS) * 3 + threadIdx.x], double(s));
+  }
+}
+
+// Last block to arrive applies `t_next` / `pending_next` to the cursor. Only READS of the cursor
+// need ordering (every block has consumed t and pending before it arrives); the data the kernel
+// wrote is published by the kernel boundary, so no release fence (an agent-scope release would
+// write back every XCD's L2 in every block).
+__device__ void cursor_arrive(uint32_t* cursor, uint32_t t_next, uint32_t pending_next, bool set_t) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int w = 0; w < PBLOCK / 64; w++) { s0 += red[0][w]; s1 += red[1][w]; s2 += red[2][w]; }
-    if (s2 > 0.f) {
-      atomicAdd(&a.stats[0], double(s0));
-      atomicAdd(&a.stats[1], double(s1));
-      atomicAdd(&a.stats[2], double(s2));
+    const uint32_t prev = __hip_atomic_fetch_add(&cursor[CUR_ARRIVED], 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      cursor[CUR_ARRIVED] = 0u;
+      if (set_t) cursor[CUR_T] = t_next;
+      cursor[CUR_PENDING] = pending_next;
     }
   }
 }
 
-__global__ void k_t_advance(uint32_t* t) { *t += 1u; }
+struct ActArgs {
+  const float* obs;         // [N,12]
+  float* act_env;           // [N,4] clipped
+  float* act;               // [T,N,4] unclipped sample or NULL
+  float* logp;              // [T,N] or NULL
+  float* value;             // [T,N] or NULL
+  float* obs_copy;          // [T,N,12] or NULL
+  const float* last_start;  // [N] or NULL
+  float* starts;            // [T,N] or NULL
+  uint32_t* cursor;         // {t, pending, arrivals} or NULL
+  int32_t rows;
+  int32_t deterministic;
+  uint64_t seed;
+  uint64_t env_base;
+  int32_t n;
+  int32_t fused;            // epilogue of step t-1 + cursor advance
+};
+
+__global__ __launch_bounds__(PBLOCK) void k_policy_act(const float* __restrict__ packed, ActArgs a, EpiArgs e) {
+  extern __shared__ float lds[];
+  stage_lds(lds, packed);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
+  const int tiles = (a.n + TILE - 1) / TILE;
+  const uint32_t t = a.cursor ? a.cursor[CUR_T] : 0u;
+  const bool pend = a.fused && a.cursor[CUR_PENDING] != 0u;
+  const uint32_t rows = uint32_t(a.rows);
+  const size_t row0 = size_t(t % rows) * a.n;
+  const size_t rowp = size_t((t + rows - 1u) % rows) * a.n;
+  const float* log_std = packed + LDS_F;
+  float st[3] = {0.f, 0.f, 0.f};
+  const int groups = (tiles + NT_ACT - 1) / NT_ACT;
+  const int stride = gridDim.x * 4;
+  int g = blockIdx.x * 4 + wave;
+  TileIn cur[NT_ACT];
+#pragma unroll
+  for (int j = 0; j < NT_ACT; j++) {
+    const int env = (g * NT_ACT + j) * TILE + (lane & 31);
+    load_tile(cur[j], a.obs, e, pend, env, g < groups && env < a.n);
+  }
+  for (; g < groups; g += stride) {
+    // issue the next group's loads now; they land while this group runs on the matrix cores
+    TileIn nxt[NT_ACT];
+#pragma unroll
+    for (int j = 0; j < NT_ACT; j++) {
+      const int env = ((g + stride) * NT_ACT + j) * TILE + (lane & 31);
+      load_tile(nxt[j], a.obs, e, pend, env, g + stride < groups && env < a.n);
+    }
+    int envs[NT_ACT];
+    bool oks[NT_ACT];
+    float ls[NT_ACT], xb[NT_ACT][6];
+#pragma unroll
+    for (int j = 0; j < NT_ACT; j++) {
+      envs[j] = (g * NT_ACT + j) * TILE + (lane & 31);
+      oks[j] = envs[j] < a.n;
+      ls[j] = 0.f;
+      if (pend) ls[j] = epilogue_tile(lds + ACTOR_F, e, cur[j], envs[j], oks[j], rowp, st);
+      else if (a.last_start && oks[j]) ls[j] = a.last_start[envs[j]];
+#pragma unroll
+      for (int s = 0; s < 6; s++) xb[j][s] = cur[j].xb[s];
+    }
+    float mean[NT_ACT][ACT], val[NT_ACT][1];
+    net_forward<ACT, NT_ACT>(lds, xb, mean);
+    net_forward<1, NT_ACT>(lds + ACTOR_F, xb, val);
+#pragma unroll
+    for (int j = 0; j < NT_ACT; j++) {
+      const int env = envs[j];
+      cur[j] = nxt[j];
+      if (!oks[j]) continue;
+      if (a.obs_copy) {
+#pragma unroll
+        for (int s = 0; s < 6; s++) a.obs_copy[(row0 + env) * OBS + 2 * s + h] = xb[j][s];
+      }
+      if (h) continue;  // one lane per env from here
+      if (a.starts) a.starts[row0 + env] = ls[j];
+      float z[ACT] = {0.f, 0.f, 0.f, 0.f};
+      if (!a.deterministic) gauss4(a.seed, a.env_base + uint64_t(env), t, z);
+      float act[ACT], lp = 0.f;
+#pragma unroll
+      for (int k = 0; k < ACT; k++) {
+        const float sd = expf(log_std[k]);
+        act[k] = mean[j][k] + sd * z[k];
+        const float zz = (act[k] - mean[j][k]) / sd;  // as PPO.train recomputes it (policy.log_prob)
+        lp += -0.5f * zz * zz - log_std[k] - 0.91893853320467274f;  // 0.5 log(2 pi)
+      }
+      reinterpret_cast<float4*>(a.act_env)[env] =
+          make_float4(fminf(fmaxf(act[0], -1.f), 1.f), fminf(fmaxf(act[1], -1.f), 1.f),
+                      fminf(fmaxf(act[2], -1.f), 1.f), fminf(fmaxf(act[3], -1.f), 1.f));
+      if (a.act) reinterpret_cast<float4*>(a.act + row0 * ACT)[env] = make_float4(act[0], act[1], act[2], act[3]);
+      if (a.logp) a.logp[row0 + env] = lp;
+      if (a.value) a.value[row0 + env] = val[j][0];
+    }
+  }
+  if (a.fused) {
+    if (pend) flush_stats(e.stats, st);
+    cursor_arrive(a.cursor, t + 1u, 1u, true);
+  }
+}
+
+__global__ __launch_bounds__(PBLOCK) void k_rollout_post(const float* __restrict__ packed, EpiArgs e,
+                                                         uint32_t* cursor, int32_t n) {
+  extern __shared__ float lds[];
+  if (cursor[CUR_PENDING] == 0u) return;  // grid-uniform: nothing to finish
+  stage_lds(lds, packed);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tiles = (n + TILE - 1) / TILE;
+  const uint32_t t = cursor[CUR_T], rows = uint32_t(e.rows);
+  const size_t rowp = size_t((t + rows - 1u) % rows) * n;
+  float st[3] = {0.f, 0.f, 0.f};
+  for (int tile = blockIdx.x * 4 + wave; tile < tiles; tile += gridDim.x * 4) {
+    const int env = tile * TILE + (lane & 31);
+    TileIn in;
+    load_tile(in, e.terminal_obs, e, true, env, env < n);  // xb unused here
+    epilogue_tile(lds + ACTOR_F, e, in, env, env < n, rowp, st);
+  }
+  flush_stats(e.stats, st);
+  cursor_arrive(cursor, 0u, 0u, false);
+}
 
 int pfail(int code, const char* m) { return set_error(code, m); }
 
-// the kernels take 149 KB of dynamic LDS (gfx950 has 160 KB per CU): opt in once per device
+// the kernels take 152 KB of dynamic LDS (gfx950 has 160 KB per CU): opt in once per device
 int lds_opt_in() {
   static bool done[64] = {};
   int dev = 0;
@@ -331,15 +487,30 @@ int lds_opt_in() {
   return QUAD_OK;
 }
 
-int grid_for(int n) {
-  const int tiles = (n + TILE - 1) / TILE;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) {
+int grid_for(int n, int nt) {
+  static int cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!cus[dev]) {
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+    cus[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
   }
-  const int want = (tiles + 3) / 4;
-  return want < cus ? want : cus;  // one 149-KB-LDS block per CU, grid-stride over tiles
+  const int groups = ((n + TILE - 1) / TILE + nt - 1) / nt;
+  const int want = (groups + 3) / 4;
+  return want < cus[dev] ? want : cus[dev];  // one LDS-filling block per CU, grid-stride over tiles
+}
+
+EpiArgs epi_args(const QuadRolloutPost* p) {
+  return EpiArgs{p->reward, p->terminated, p->truncated, p->terminal_obs, p->buf_rew, p->last_start,
+                 p->ep_ret, p->ep_len, p->stats, p->rows, p->gamma};
+}
+
+int check_epi(const QuadRolloutPost* p) {
+  if (!p->reward || !p->terminated || !p->truncated || !p->terminal_obs || !p->buf_rew ||
+      !p->last_start || !p->ep_ret || !p->ep_len || !p->stats)
+    return pfail(QUAD_EINVAL, "rollout epilogue: NULL buffer");
+  if (p->rows < 1) return pfail(QUAD_EINVAL, "rollout epilogue: rows must be >= 1");
+  return QUAD_OK;
 }
 
 }  // namespace
@@ -350,8 +521,11 @@ int32_t quad_policy_packed_floats(void) { return PACKED_F; }
 
 int quad_policy_pack(const QuadPolicyParams* p, float* packed, void* stream) {
   if (!p || !packed) return pfail(QUAD_EINVAL, "params/packed is NULL");
-  if (int rc = lds_opt_in()) return rc;
+  if (!p->pi_w0 || !p->pi_b0 || !p->pi_w1 || !p->pi_b1 || !p->act_w || !p->act_b || !p->vf_w0 ||
+      !p->vf_b0 || !p->vf_w1 || !p->vf_b1 || !p->val_w || !p->val_b || !p->log_std)
+    return pfail(QUAD_EINVAL, "a policy parameter pointer is NULL");
   if (reinterpret_cast<uintptr_t>(packed) & 15u) return pfail(QUAD_EINVAL, "packed must be 16-byte aligned");
+  if (int rc = lds_opt_in()) return rc;
   NetPtrs actor{p->pi_w0, p->pi_b0, p->pi_w1, p->pi_b1, p->act_w, p->act_b};
   NetPtrs critic{p->vf_w0, p->vf_b0, p->vf_w1, p->vf_b1, p->val_w, p->val_b};
   hipLaunchKernelGGL(k_policy_pack, dim3((PACKED_F + 255) / 256), dim3(256), 0,
@@ -362,31 +536,35 @@ int quad_policy_pack(const QuadPolicyParams* p, float* packed, void* stream) {
 int quad_policy_act(const float* packed, const QuadPolicyAct* s, int32_t n, void* stream) {
   if (!packed || !s || !s->obs || !s->actions_env) return pfail(QUAD_EINVAL, "NULL argument");
   if (n <= 0) return pfail(QUAD_EINVAL, "n must be > 0");
-  if ((reinterpret_cast<uintptr_t>(s->actions_env) | reinterpret_cast<uintptr_t>(s->actions)) & 15u)
-    return pfail(QUAD_EINVAL, "action buffers must be 16-byte aligned");
   if (s->rows < 1) return pfail(QUAD_EINVAL, "rows must be >= 1");
+  if ((reinterpret_cast<uintptr_t>(packed) | reinterpret_cast<uintptr_t>(s->actions_env) |
+       reinterpret_cast<uintptr_t>(s->actions)) & 15u)
+    return pfail(QUAD_EINVAL, "packed and action buffers must be 16-byte aligned");
+  EpiArgs e{};
+  if (s->epilogue) {
+    if (!s->cursor) return pfail(QUAD_EINVAL, "a fused epilogue needs the cursor");
+    if (int rc = check_epi(s->epilogue)) return rc;
+    if (s->epilogue->rows != s->rows) return pfail(QUAD_EINVAL, "epilogue rows != rows");
+    e = epi_args(s->epilogue);
+  }
   if (int rc = lds_opt_in()) return rc;
-  ActArgs a{s->obs, s->actions_env, s->actions, s->log_prob, s->value, s->obs_copy,
-            s->last_start, s->episode_starts, s->t_index, s->rows,
-            s->seed, s->env_id_base, n, s->deterministic};
-  hipLaunchKernelGGL(k_policy_act, dim3(grid_for(n)), dim3(PBLOCK), LDS_F * sizeof(float),
-                     static_cast<hipStream_t>(stream), packed, a);
+  ActArgs a{s->obs, s->actions_env, s->actions, s->log_prob, s->value, s->obs_copy, s->last_start,
+            s->episode_starts, s->cursor, s->rows, s->deterministic, s->seed, s->env_id_base, n,
+            s->epilogue ? 1 : 0};
+  hipLaunchKernelGGL(k_policy_act, dim3(grid_for(n, NT_ACT)), dim3(PBLOCK), LDS_F * sizeof(float),
+                     static_cast<hipStream_t>(stream), packed, a, e);
   return hipGetLastError() == hipSuccess ? QUAD_OK : pfail(QUAD_EHIP, "k_policy_act launch failed");
 }
 
-int quad_rollout_post(const float* packed, const QuadRolloutPost* s, int32_t n, void* stream) {
-  if (!packed || !s || !s->reward || !s->terminated || !s->truncated || !s->terminal_obs ||
-      !s->buf_rew || !s->last_start || !s->ep_ret || !s->ep_len || !s->stats || !s->t_index)
-    return pfail(QUAD_EINVAL, "NULL argument");
+int quad_rollout_post(const float* packed, const QuadRolloutPost* p, uint32_t* cursor, int32_t n,
+                      void* stream) {
+  if (!packed || !p || !cursor) return pfail(QUAD_EINVAL, "NULL argument");
   if (n <= 0) return pfail(QUAD_EINVAL, "n must be > 0");
-  if (s->rows < 1) return pfail(QUAD_EINVAL, "rows must be >= 1");
+  if (reinterpret_cast<uintptr_t>(packed) & 15u) return pfail(QUAD_EINVAL, "packed must be 16-byte aligned");
+  if (int rc = check_epi(p)) return rc;
   if (int rc = lds_opt_in()) return rc;
-  PostArgs a{s->reward, s->terminated, s->truncated, s->terminal_obs, s->buf_rew, s->last_start,
-             s->ep_ret, s->ep_len, s->stats, s->t_index, s->rows, s->gamma, n};
-  const int tiles = (n + TILE - 1) / TILE;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(k_rollout_post, dim3((tiles + 3) / 4), dim3(PBLOCK), LDS_F * sizeof(float), st, packed, a);
-  hipLaunchKernelGGL(k_t_advance, dim3(1), dim3(1), 0, st, s->t_index);
+  hipLaunchKernelGGL(k_rollout_post, dim3(grid_for(n, 1)), dim3(PBLOCK), LDS_F * sizeof(float),
+                     static_cast<hipStream_t>(stream), packed, epi_args(p), cursor, n);
   return hipGetLastError() == hipSuccess ? QUAD_OK : pfail(QUAD_EHIP, "k_rollout_post launch failed");
 }
 

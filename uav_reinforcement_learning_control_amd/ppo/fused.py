@@ -62,9 +62,12 @@ class FusedPolicy:
 
     def act(self, obs: torch.Tensor, actions_env: torch.Tensor, *, actions=None, log_prob=None,
             value=None, obs_copy=None, last_start=None, episode_starts=None,
-            t_index: Optional[torch.Tensor] = None, rows: int = 1, seed: int = 0,
-            env_id_base: int = 0, deterministic: bool = False) -> None:
-        """quad_policy_act: row buffers are [rows, N, ...] (row t % rows, t = t_index[0])."""
+            cursor: Optional[torch.Tensor] = None, rows: int = 1, seed: int = 0,
+            env_id_base: int = 0, deterministic: bool = False,
+            epilogue: Optional[N.QuadRolloutPost] = None) -> None:
+        """quad_policy_act: row buffers are [rows, N, ...] (row t % rows, t = cursor[0]); with
+        `epilogue` (from make_epilogue) the pending previous step is finished in the same launch
+        and the cursor advances."""
         n, dev, f32 = obs.shape[0], self.device, torch.float32
         _need(obs, (n, 12), f32, dev, "obs")
         _need(actions_env, (n, 4), f32, dev, "actions_env")
@@ -73,19 +76,20 @@ class FusedPolicy:
                              (last_start, (n,), "last_start"), (episode_starts, (rows, n), "episode_starts")):
             if t is not None:
                 _need(t, shp, f32, dev, name)
-        if t_index is not None:
-            _need(t_index, (1,), torch.int32, dev, "t_index")
+        if cursor is not None:
+            _need(cursor, (4,), torch.int32, dev, "cursor")
         a = N.QuadPolicyAct(obs=obs.data_ptr(), actions_env=actions_env.data_ptr(),
                             actions=_p(actions), log_prob=_p(log_prob), value=_p(value),
                             obs_copy=_p(obs_copy), last_start=_p(last_start),
-                            episode_starts=_p(episode_starts), t_index=_p(t_index), rows=int(rows),
+                            episode_starts=_p(episode_starts), cursor=_p(cursor), rows=int(rows),
                             deterministic=int(bool(deterministic)), seed=int(seed) & (2**64 - 1),
-                            env_id_base=int(env_id_base))
+                            env_id_base=int(env_id_base),
+                            epilogue=C.pointer(epilogue) if epilogue is not None else None)
         N.check(N.lib().quad_policy_act(_p(self.packed), C.byref(a), n, self._stream()), "quad_policy_act")
 
-    def post(self, reward, terminated, truncated, terminal_obs, buf_rew, last_start, ep_ret, ep_len,
-             stats, t_index, rows: int, gamma: float) -> None:
-        """quad_rollout_post (then t_index += 1)."""
+    def make_epilogue(self, reward, terminated, truncated, terminal_obs, buf_rew, last_start, ep_ret,
+                      ep_len, stats, rows: int, gamma: float) -> N.QuadRolloutPost:
+        """The QuadRolloutPost of a rollout (buffers are referenced, not copied: keep them alive)."""
         n, dev, f32 = reward.shape[0], self.device, torch.float32
         _need(reward, (n,), f32, dev, "reward")
         _need(terminated, (n,), torch.bool, dev, "terminated")
@@ -94,13 +98,17 @@ class FusedPolicy:
         _need(buf_rew, (rows, n), f32, dev, "buf_rew")
         for t, name in ((last_start, "last_start"), (ep_ret, "ep_ret"), (ep_len, "ep_len")):
             _need(t, (n,), f32, dev, name)
-        _need(stats, (3,), torch.float64, dev, "stats")
-        _need(t_index, (1,), torch.int32, dev, "t_index")
-        p = N.QuadRolloutPost(reward=reward.data_ptr(), terminated=terminated.data_ptr(),
+        _need(stats, (N.POLICY_STAT_SLOTS, 3), torch.float64, dev, "stats")
+        e = N.QuadRolloutPost(reward=reward.data_ptr(), terminated=terminated.data_ptr(),
                               truncated=truncated.data_ptr(), terminal_obs=terminal_obs.data_ptr(),
                               buf_rew=buf_rew.data_ptr(), last_start=last_start.data_ptr(),
                               ep_ret=ep_ret.data_ptr(), ep_len=ep_len.data_ptr(),
-                              stats=stats.data_ptr(), t_index=t_index.data_ptr(), rows=int(rows),
-                              gamma=float(gamma))
-        N.check(N.lib().quad_rollout_post(_p(self.packed), C.byref(p), n, self._stream()),
-                "quad_rollout_post")
+                              stats=stats.data_ptr(), rows=int(rows), gamma=float(gamma))
+        e._n = n
+        return e
+
+    def post(self, epilogue: N.QuadRolloutPost, cursor: torch.Tensor) -> None:
+        """quad_rollout_post: finish the pending step (end of a rollout)."""
+        _need(cursor, (4,), torch.int32, self.device, "cursor")
+        N.check(N.lib().quad_rollout_post(_p(self.packed), C.byref(epilogue), _p(cursor), epilogue._n,
+                                          self._stream()), "quad_rollout_post")

@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from .. import _native as N
 from .fused import FusedPolicy
 from .gae import gae
 from .policy import ActorCritic
@@ -132,9 +133,15 @@ class PPO:
         self._act_env = torch.zeros(n, 4, **f32)
         self._done_stats = torch.zeros(3, dtype=torch.float64, device=self.device)
         self._graph = None
-        # fused path: running step counter (buffer row = t % n_steps; keys the action noise)
+        # fused path: cursor {t, pending} (buffer row = t % n_steps; t keys the action noise),
+        # per-block episode-statistic slots, the epilogue descriptor
         self._fp = FusedPolicy(self.policy) if self.cfg.fused_policy else None
-        self._tc = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._cursor = torch.zeros(4, dtype=torch.int32, device=self.device)
+        self._slots = torch.zeros(N.POLICY_STAT_SLOTS, 3, dtype=torch.float64, device=self.device)
+        if self._fp is not None:
+            self._epi = self._fp.make_epilogue(env.reward, env.terminated, env.truncated,
+                                               env.terminal_obs, self.buf_rew, self.last_start,
+                                               self.ep_ret, self.ep_len, self._slots, T, self.cfg.gamma)
         self._noise_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5851F42D4C957F2D) & (2**64 - 1)
 
     # ------------------------------------------------------------------------------------
@@ -171,15 +178,14 @@ class PPO:
         self._t += 1
 
     def _rollout_step_fused(self):
-        """The same step as three launches: MFMA policy, env, epilogue (graph-capturable)."""
-        env, T = self.env, self.cfg.n_steps
+        """The same step as two launches (graph-capturable): the MFMA policy kernel, which also
+        finishes the previous step (bootstrap, reward row, statistics), and the env step."""
+        env = self.env
         self._fp.act(self.last_obs, self._act_env, actions=self.buf_act, log_prob=self.buf_logp,
                      value=self.buf_val, obs_copy=self.buf_obs, last_start=self.last_start,
-                     episode_starts=self.buf_start, t_index=self._tc, rows=T,
-                     seed=self._noise_seed, env_id_base=env.env_id_base)
-        _, rew, term, trunc, info = env.step(self._act_env, obs=self.last_obs, info="raw")
-        self._fp.post(rew, term, trunc, info["terminal_observation"], self.buf_rew, self.last_start,
-                      self.ep_ret, self.ep_len, self._done_stats, self._tc, T, self.cfg.gamma)
+                     episode_starts=self.buf_start, cursor=self._cursor, rows=self.cfg.n_steps,
+                     seed=self._noise_seed, env_id_base=env.env_id_base, epilogue=self._epi)
+        env.step(self._act_env, obs=self.last_obs, info="raw")
 
     def _step_fn(self):
         return self._rollout_step_fused if self._fp is not None else self._rollout_step
@@ -193,7 +199,7 @@ class PPO:
             step()
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._t.zero_()
-        self._tc.zero_()
+        self._cursor.zero_()
         self._graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._graph):
             step()
@@ -214,11 +220,15 @@ class PPO:
         self._t.zero_()
         self._done_stats.zero_()
         step = self._step_fn()
+        self._slots.zero_()
         for _ in range(cfg.n_steps):
             if use_graph and self._graph is not None:
                 self._graph.replay()
             else:
                 step()
+        if self._fp is not None:
+            self._fp.post(self._epi, self._cursor)   # finish the last step
+            self._done_stats.copy_(self._slots.sum(0))
         last_v = pol.value(self.last_obs)
         gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
             cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
