@@ -35,8 +35,7 @@ namespace {
 
 constexpr int H = 128, OBS = 12, ACT = 4;
 constexpr int TILE = 32;     // envs per MFMA tile (one wave holds one tile at a time)
-constexpr int PBLOCK = 256;  // 4 waves
-constexpr int NT_ACT = 2;    // tiles per wave iteration in k_policy_act (shared weight fragments)
+constexpr int PBLOCK = 256;  // 4 waves (k_rollout_post; k_policy_act takes BLK)
 
 // packed net image (floats); NOUT = 4 (actor) or 1 (critic):
 //   W1: [4 n][64 lane][8]              layer-1 A fragments, k-steps s = 0..5 (6, 7 zero)
@@ -119,6 +118,34 @@ __device__ __forceinline__ void bias_init(f32x16& acc, const float* L, int off) 
   }
 }
 
+// 1/16 of one 32-neuron block's head: ReLU of accumulator register(s) `i` (actor: register i; critic:
+// registers 4(i/4).. handled at i % 4 == 0) times the packed head weights, into part[][].
+template <int NOUT, int NT>
+__device__ __forceinline__ void head_part(const float* __restrict__ L, const f32x16 (&x)[NT], int m, int i,
+                                          int h, float (&part)[NT][NOUT]) {
+  if constexpr (NOUT == ACT) {
+    const float4 w = ld4(L, NET_W3 + ((m * 16 + i) * 2 + h) * 4);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      const float v = fmaxf(x[j][i], 0.f);
+      part[j][0] = fmaf(w.x, v, part[j][0]);
+      part[j][1] = fmaf(w.y, v, part[j][1]);
+      part[j][2] = fmaf(w.z, v, part[j][2]);
+      part[j][3] = fmaf(w.w, v, part[j][3]);
+    }
+  } else {
+    if (i % 4 != 0) return;
+    const float4 w = ld4(L, NET_W3 + ((m * 4 + i / 4) * 2 + h) * 4);
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      part[j][0] = fmaf(w.x, fmaxf(x[j][i + 0], 0.f), part[j][0]);
+      part[j][0] = fmaf(w.y, fmaxf(x[j][i + 1], 0.f), part[j][0]);
+      part[j][0] = fmaf(w.z, fmaxf(x[j][i + 2], 0.f), part[j][0]);
+      part[j][0] = fmaf(w.w, fmaxf(x[j][i + 3], 0.f), part[j][0]);
+    }
+  }
+}
+
 // ---- one net's forward for NT 32-env tiles at once (all 64 lanes). X^T fragments:
 // xb[j][s] = x[env = lane&31 of tile j][2 s + (lane>>5)]. Returns the NOUT head outputs of env
 // lane&31 of every tile (both lane halves get them). The NT tiles share every LDS weight fragment,
@@ -153,53 +180,42 @@ __device__ __forceinline__ void net_forward(const float* __restrict__ L, const f
   for (int j = 0; j < NT; j++)
 #pragma unroll
     for (int o = 0; o < NOUT; o++) part[j][o] = 0.f;
+  // Layer 2 in four 32-neuron blocks m. The VALU head of block m-1 is issued inside block m's MFMA
+  // chain (independent work), so it runs in the matrix pipe's shadow instead of after it.
+  f32x16 prev[NT];  // block m-1 (zeros before block 0: its head then adds exact zeros)
+#pragma unroll
+  for (int j = 0; j < NT; j++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) prev[j][r] = 0.f;
 #pragma unroll 1
   for (int m = 0; m < 4; m++) {
     f32x16 acc[NT];
     bias_init(acc[0], L, NET_B2 + (m * 2 + h) * 16);
 #pragma unroll
     for (int j = 1; j < NT; j++) acc[j] = acc[0];
+    // A fragments double-buffered: fragment i+1 is in flight while the MFMAs of fragment i issue
+    // (one register quad would make each ds_read wait for the last MFMA that reads it)
+    const int wbase = NET_W2 + (m * 16 * 64 + lane) * 4;
+    float4 a4 = ld4(L, wbase);
 #pragma unroll
-    for (int n = 0; n < 4; n++) {
+    for (int i = 0; i < 16; i++) {  // i = 4 n + q
+      const int n = i / 4, q = i % 4;
+      float4 nx;
+      if (i < 15) nx = ld4(L, wbase + (i + 1) * 64 * 4);
+      const float w[4] = {a4.x, a4.y, a4.z, a4.w};
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const float4 a4 = ld4(L, NET_W2 + (((m * 4 + n) * 4 + q) * 64 + lane) * 4);
-        const float w[4] = {a4.x, a4.y, a4.z, a4.w};
+      for (int k = 0; k < 4; k++)
 #pragma unroll
-        for (int k = 0; k < 4; k++)
-#pragma unroll
-          for (int j = 0; j < NT; j++)
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[k], h1[j][n][4 * q + k], acc[j], 0, 0, 0);
-      }
+        for (int j = 0; j < NT; j++)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[k], h1[j][n][4 * q + k], acc[j], 0, 0, 0);
+      head_part<NOUT, NT>(L, prev, m > 0 ? m - 1 : 0, i, h, part);  // 1/16 of block m-1's head
+      if (i < 15) a4 = nx;
     }
-    // ReLU, then this 32-neuron slice's contribution to the head (VALU)
-    if constexpr (NOUT == ACT) {
 #pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const float4 w = ld4(L, NET_W3 + ((m * 16 + r) * 2 + h) * 4);
-#pragma unroll
-        for (int j = 0; j < NT; j++) {
-          const float x = fmaxf(acc[j][r], 0.f);
-          part[j][0] = fmaf(w.x, x, part[j][0]);
-          part[j][1] = fmaf(w.y, x, part[j][1]);
-          part[j][2] = fmaf(w.z, x, part[j][2]);
-          part[j][3] = fmaf(w.w, x, part[j][3]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int rq = 0; rq < 4; rq++) {
-        const float4 w = ld4(L, NET_W3 + ((m * 4 + rq) * 2 + h) * 4);
-#pragma unroll
-        for (int j = 0; j < NT; j++) {
-          part[j][0] = fmaf(w.x, fmaxf(acc[j][4 * rq + 0], 0.f), part[j][0]);
-          part[j][0] = fmaf(w.y, fmaxf(acc[j][4 * rq + 1], 0.f), part[j][0]);
-          part[j][0] = fmaf(w.z, fmaxf(acc[j][4 * rq + 2], 0.f), part[j][0]);
-          part[j][0] = fmaf(w.w, fmaxf(acc[j][4 * rq + 3], 0.f), part[j][0]);
-        }
-      }
-    }
+    for (int j = 0; j < NT; j++) prev[j] = acc[j];
   }
+#pragma unroll
+  for (int i = 0; i < 16; i++) head_part<NOUT, NT>(L, prev, 3, i, h, part);
   // lanes l and l ^ 32 hold the two halves of the same env's neurons; both lanes form the same sum
 #pragma unroll
   for (int j = 0; j < NT; j++)
@@ -212,8 +228,9 @@ __device__ __forceinline__ void net_forward(const float* __restrict__ L, const f
 
 // 152 KB global -> LDS per block: batches of 13 float4 loads in flight per thread (a serial
 // load -> store loop would pay ~38 round trips of L2/MALL latency)
+template <int BLK>
 __device__ __forceinline__ void stage_lds(float* lds, const float* __restrict__ packed) {
-  constexpr int NV = LDS_F / 4, PER = (NV + PBLOCK - 1) / PBLOCK, BATCH = 13;
+  constexpr int NV = LDS_F / 4, PER = (NV + BLK - 1) / BLK, BATCH = BLK >= 512 ? 10 : 13;
   const float4* src = reinterpret_cast<const float4*>(packed);
   float4* dst = reinterpret_cast<float4*>(lds);
 #pragma unroll
@@ -221,12 +238,12 @@ __device__ __forceinline__ void stage_lds(float* lds, const float* __restrict__ 
     float4 v[BATCH];
 #pragma unroll
     for (int j = 0; j < BATCH; j++) {
-      const int k = (b0 + j) * PBLOCK + threadIdx.x;
+      const int k = (b0 + j) * BLK + threadIdx.x;
       v[j] = src[k < NV ? k : NV - 1];  // clamped: every element defined, stays in VGPRs
     }
 #pragma unroll
     for (int j = 0; j < BATCH; j++) {
-      const int k = (b0 + j) * PBLOCK + threadIdx.x;
+      const int k = (b0 + j) * BLK + threadIdx.x;
       if (b0 + j < PER && k < NV) dst[k] = v[j];
     }
   }
@@ -317,8 +334,9 @@ __device__ __forceinline__ float epilogue_tile(const float* __restrict__ Lc, con
 }
 
 // block-reduce the episode statistics into this block's slot (uncontended atomics)
+template <int BLK>
 __device__ void flush_stats(double* stats, float st[3]) {
-  __shared__ float red[3][PBLOCK / 64];
+  __shared__ float red[3][BLK / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int j = 0; j < 3; j++) {
@@ -329,7 +347,7 @@ __device__ void flush_stats(double* stats, float st[3]) {
   __syncthreads();
   if (threadIdx.x < 3) {
     float s = 0.f;
-    for (int w = 0; w < PBLOCK / 64; w++) s += red[threadIdx.x][w];
+    for (int w = 0; w < BLK / 64; w++) s += red[threadIdx.x][w];
     if (s != 0.f) atomicAdd(&stats[(blockIdx.x % QUAD_POLICY_STAT_SLOTS) * 3 + threadIdx.x], double(s));
   }
 }
@@ -369,9 +387,13 @@ struct ActArgs {
   int32_t fused;            // epilogue of step t-1 + cursor advance
 };
 
-__global__ __launch_bounds__(PBLOCK) void k_policy_act(const float* __restrict__ packed, ActArgs a, EpiArgs e) {
+// NT_ACT tiles per wave iteration (sharing weight fragments), BLK threads per block (one block per
+// CU; BLK = 512 puts two waves on each SIMD, which caps a wave at 256 registers)
+template <int NT_ACT, int BLK>
+__global__ __launch_bounds__(BLK) void k_policy_act(const float* __restrict__ packed, ActArgs a, EpiArgs e) {
   extern __shared__ float lds[];
-  stage_lds(lds, packed);
+  constexpr int WAVES = BLK / 64;
+  stage_lds<BLK>(lds, packed);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, h = lane >> 5;
   const int tiles = (a.n + TILE - 1) / TILE;
   const uint32_t t = a.cursor ? a.cursor[CUR_T] : 0u;
@@ -382,8 +404,8 @@ __global__ __launch_bounds__(PBLOCK) void k_policy_act(const float* __restrict__
   const float* log_std = packed + LDS_F;
   float st[3] = {0.f, 0.f, 0.f};
   const int groups = (tiles + NT_ACT - 1) / NT_ACT;
-  const int stride = gridDim.x * 4;
-  int g = blockIdx.x * 4 + wave;
+  const int stride = gridDim.x * WAVES;
+  int g = blockIdx.x * WAVES + wave;
   TileIn cur[NT_ACT];
 #pragma unroll
   for (int j = 0; j < NT_ACT; j++) {
@@ -444,7 +466,7 @@ __global__ __launch_bounds__(PBLOCK) void k_policy_act(const float* __restrict__
     }
   }
   if (a.fused) {
-    if (pend) flush_stats(e.stats, st);
+    if (pend) flush_stats<BLK>(e.stats, st);
     cursor_arrive(a.cursor, t + 1u, 1u, true);
   }
 }
@@ -453,7 +475,7 @@ __global__ __launch_bounds__(PBLOCK) void k_rollout_post(const float* __restrict
                                                          uint32_t* cursor, int32_t n) {
   extern __shared__ float lds[];
   if (cursor[CUR_PENDING] == 0u) return;  // grid-uniform: nothing to finish
-  stage_lds(lds, packed);
+  stage_lds<PBLOCK>(lds, packed);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tiles = (n + TILE - 1) / TILE;
   const uint32_t t = cursor[CUR_T], rows = uint32_t(e.rows);
@@ -465,7 +487,7 @@ __global__ __launch_bounds__(PBLOCK) void k_rollout_post(const float* __restrict
     load_tile(in, e.terminal_obs, e, true, env, env < n);  // xb unused here
     epilogue_tile(lds + ACTOR_F, e, in, env, env < n, rowp, st);
   }
-  flush_stats(e.stats, st);
+  flush_stats<PBLOCK>(e.stats, st);
   cursor_arrive(cursor, 0u, 0u, false);
 }
 
@@ -478,8 +500,9 @@ int lds_opt_in() {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return pfail(QUAD_EHIP, "hipGetDevice failed");
   if (done[dev]) return QUAD_OK;
   const int bytes = LDS_F * int(sizeof(float));
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_policy_act),
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_policy_act<2, 256>),
                           hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess ||
+
       hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rollout_post),
                           hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
     return pfail(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
@@ -487,7 +510,7 @@ int lds_opt_in() {
   return QUAD_OK;
 }
 
-int grid_for(int n, int nt) {
+int grid_for(int n, int nt, int waves) {
   static int cus[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
@@ -496,7 +519,7 @@ int grid_for(int n, int nt) {
     cus[dev] = hipGetDeviceProperties(&prop, dev) == hipSuccess ? prop.multiProcessorCount : 256;
   }
   const int groups = ((n + TILE - 1) / TILE + nt - 1) / nt;
-  const int want = (groups + 3) / 4;
+  const int want = (groups + waves - 1) / waves;
   return want < cus[dev] ? want : cus[dev];  // one LDS-filling block per CU, grid-stride over tiles
 }
 
@@ -551,7 +574,9 @@ int quad_policy_act(const float* packed, const QuadPolicyAct* s, int32_t n, void
   ActArgs a{s->obs, s->actions_env, s->actions, s->log_prob, s->value, s->obs_copy, s->last_start,
             s->episode_starts, s->cursor, s->rows, s->deterministic, s->seed, s->env_id_base, n,
             s->epilogue ? 1 : 0};
-  hipLaunchKernelGGL(k_policy_act, dim3(grid_for(n, NT_ACT)), dim3(PBLOCK), LDS_F * sizeof(float),
+  // 2 tiles per wave, 4 waves per CU: measured best (8-wave blocks cap a wave at 256 registers and
+  // spill)
+  hipLaunchKernelGGL((k_policy_act<2, 256>), dim3(grid_for(n, 2, 4)), dim3(256), LDS_F * sizeof(float),
                      static_cast<hipStream_t>(stream), packed, a, e);
   return hipGetLastError() == hipSuccess ? QUAD_OK : pfail(QUAD_EHIP, "k_policy_act launch failed");
 }
@@ -563,7 +588,7 @@ int quad_rollout_post(const float* packed, const QuadRolloutPost* p, uint32_t* c
   if (reinterpret_cast<uintptr_t>(packed) & 15u) return pfail(QUAD_EINVAL, "packed must be 16-byte aligned");
   if (int rc = check_epi(p)) return rc;
   if (int rc = lds_opt_in()) return rc;
-  hipLaunchKernelGGL(k_rollout_post, dim3(grid_for(n, 1)), dim3(PBLOCK), LDS_F * sizeof(float),
+  hipLaunchKernelGGL(k_rollout_post, dim3(grid_for(n, 1, 4)), dim3(PBLOCK), LDS_F * sizeof(float),
                      static_cast<hipStream_t>(stream), packed, epi_args(p), cursor, n);
   return hipGetLastError() == hipSuccess ? QUAD_OK : pfail(QUAD_EHIP, "k_rollout_post launch failed");
 }
