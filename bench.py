@@ -116,6 +116,13 @@ def _run_rank(args, rank, world, local_rank):
                event_pair_us=_kernel_time_us(env, step, actions, args.kernel_launches))
     if args.rollout_steps > 0:
         res["rollout"] = _rollout_phase(env, args)
+    if args.e2e_iters > 0:
+        res["end_to_end"] = _end_to_end(env, args)
+    if rank == 0 and not args.no_configs:
+        res["configs"] = {
+            "config2_hover_4096": _kernel_rate(4096, "hover", None, dev, args.seed),
+            "config5_traj_ctbr_65536": _kernel_rate(65536, "trajectory", "RateControlWrapper", dev, args.seed),
+            "hover_ctbr_65536": _kernel_rate(65536, "hover", "RateControlWrapper", dev, args.seed)}
     if rank == 0 and args.large_envs > 0:
         del actions, g
         env.close()
@@ -144,6 +151,61 @@ def _run_rank(args, rank, world, local_rank):
     return res
 
 
+def _kernel_rate(n, kind, wrapper, dev, seed) -> dict:
+    """Env-step kernel time for another SURVEY 8(d) config (graph of 20 launches, 10 replays)."""
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    e = QuadVecEnv(n, env=kind, wrapper=wrapper, device=dev, seed=seed)
+    e.reset()
+    acts = [e.random_actions(k) for k in range(4)]
+    st = _quad_step_fn(e)
+    for k in range(50):
+        st(acts[k % 4].data_ptr())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for k in range(20):
+            st(acts[k % 4].data_ptr())
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / 200
+    e.close()
+    bpe = BYTES_PER_ENV_STEP + (24 if wrapper else 0)
+    return {"envs": n, "env": kind, "wrapper": wrapper, "kernel_us": us,
+            "env_steps_per_s": n / (us * 1e-6), "achieved_GBs": bpe * n / (us * 1e-6) / 1e9}
+
+
+def _end_to_end(env, args) -> dict:
+    """One full PPO iteration per SURVEY 8(d) config 3: rollout of n_steps (MFMA policy path) +
+    GAE + the SB3-schedule update (n_epochs x n_minibatches Adam steps on the rollout buffer)."""
+    from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
+    cfg = PPOConfig(n_steps=args.e2e_steps, n_epochs=args.e2e_epochs)
+    m = PPO(env, cfg, seed=0)
+    m.collect_rollouts(use_graph=True)  # capture + warm (not timed)
+    m.train(n_epochs=1, max_minibatches=2)
+    torch.cuda.synchronize()
+    t_roll = t_train = 0.0
+    for _ in range(args.e2e_iters):
+        rs = m.collect_rollouts(use_graph=True)
+        t0 = time.perf_counter()
+        m.train()
+        torch.cuda.synchronize()
+        t_train += time.perf_counter() - t0
+        t_roll += rs.seconds
+    steps = args.e2e_iters * rs.env_steps
+    out = {"n_steps": cfg.n_steps, "n_epochs": cfg.n_epochs, "minibatches_per_epoch": cfg.n_minibatches,
+           "minibatch": m.batch, "iterations": args.e2e_iters,
+           "rollout_s": t_roll / args.e2e_iters, "train_s": t_train / args.e2e_iters,
+           "env_steps_per_s": steps / (t_roll + t_train)}
+    del m
+    torch.cuda.empty_cache()
+    return out
+
+
 def _rollout_phase(env, args) -> dict:
     """PPO rollout phase on the same 65,536 envs, one hipGraph per rollout step, GAE included,
     timed over n_steps: the MFMA policy path (policy kernel + env step + epilogue = 3 launches)
@@ -158,6 +220,23 @@ def _rollout_phase(env, args) -> dict:
         rs = m.collect_rollouts(use_graph=True)
         out[name] = {"env_steps_per_s": rs.env_steps / rs.seconds,
                      "ms_per_step": rs.seconds / args.rollout_steps * 1e3}
+        if fused:  # the policy kernel alone (HIP events on its stream): MFMA roofline
+            n = env.num_envs
+            ae = torch.empty(n, 4, device=env.device)
+            for _ in range(5):
+                m._fp.act(m.last_obs, ae, seed=1)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(100):
+                m._fp.act(m.last_obs, ae, seed=1)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / 100
+            flop = n * (2 * 2 * (12 * 128 + 128 * 128) + 2 * 128 * 5)
+            out["policy_kernel"] = {"kernel": "k_policy_act<2,256>", "kernel_us": us,
+                                    "flop_per_launch": flop, "achieved_TFLOPs": flop / (us * 1e-6) / 1e12,
+                                    "peak_TFLOPs": 157.3, "bound": "mfma (fp32 32x32x2)"}
         del m
         torch.cuda.empty_cache()
     out["env_steps_per_s"] = out["mfma"]["env_steps_per_s"]
@@ -209,6 +288,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--rollout-steps", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs", action="store_true")
+    ap.add_argument("--e2e-iters", type=int, default=1)
+    ap.add_argument("--e2e-steps", type=int, default=1024)
+    ap.add_argument("--e2e-epochs", type=int, default=20)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -248,6 +331,12 @@ def main():
     }
     if "rollout" in res:
         line["rollout_phase"] = res["rollout"]
+    if "end_to_end" in res:
+        e = dict(res["end_to_end"])
+        e["env_steps_per_s"] *= world
+        line["end_to_end"] = e
+    if "configs" in res:
+        line["configs"] = res["configs"]
     if "large_kernel_us" in res:
         lk = res["large_kernel_us"]
         line["large_batch"] = {"envs": args.large_envs, "kernel_us": lk,

@@ -21,5 +21,5 @@ STEPS=${STEPS:-pytest,smoke,bench,prof}
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py
 [[ $STEPS == *sweep* ]] && run sweep 600 python tools/lanes_sweep.py
-[[ $STEPS == *prof* ]] && run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --steps 1000
+[[ $STEPS == *prof* ]] && run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --no-cpu-baseline --e2e-iters 0 --no-configs
 echo "=== done"
