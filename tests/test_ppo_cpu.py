@@ -121,3 +121,21 @@ def test_gradient_allreduce_two_ranks_gloo():
     mean = (res[0][0] + res[1][0]) / 2
     np.testing.assert_allclose(res[0][1], mean, rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(res[1][1], mean, rtol=1e-6, atol=1e-7)
+
+
+def test_split_k_linear_gradients_match_plain():
+    """The split-K weight gradient (tall PPO minibatches) equals the plain one to fp32 rounding."""
+    import torch.nn as nn
+    from uav_reinforcement_learning_control_amd.ppo import policy as P
+    torch.manual_seed(0)
+    lin = nn.Linear(12, 128)
+    x = torch.randn(65536 * 2, 12, requires_grad=True)
+    y = P._linear(x, lin)
+    assert P._chunks(x.shape[0]) == 32
+    g = torch.randn_like(y)
+    gx, gw, gb = torch.autograd.grad(y, (x, lin.weight, lin.bias), g)
+    y2 = torch.nn.functional.linear(x, lin.weight, lin.bias)
+    gx2, gw2, gb2 = torch.autograd.grad(y2, (x, lin.weight, lin.bias), g)
+    assert torch.equal(y, y2) and torch.allclose(gx, gx2, atol=1e-5)
+    assert torch.allclose(gw, gw2, rtol=1e-4, atol=1e-3) and torch.allclose(gb, gb2, rtol=1e-4, atol=1e-3)
+    assert P._chunks(100_000) == 16 and P._chunks(3) == 1

@@ -15,6 +15,53 @@ import torch
 import torch.nn as nn
 
 
+class _SplitKLinear(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient is split over row chunks.
+
+    PPO minibatches are tall (524,288 rows at the default schedule) while W is at most 128 x 128,
+    so dW = dY^T X is a GEMM with a tiny output and a huge K; the BLAS picks un-split tiles for it
+    (~1 ms each on MI355X). Chunking K into C slabs of ~4k rows turns it into a batched GEMM with
+    C x the parallelism plus a cheap reduction over C.
+    """
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        return torch.nn.functional.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        m = gy.shape[0]
+        c = _chunks(m)
+        if c > 1:
+            gw = torch.bmm(gy.reshape(c, m // c, -1).transpose(1, 2), x.reshape(c, m // c, -1)).sum(0)
+        else:
+            gw = gy.t() @ x
+        return gx, gw, gy.sum(0)
+
+
+def _chunks(m: int, rows: int = 4096) -> int:
+    """Largest power-of-two chunk count with >= `rows` rows per chunk that divides m."""
+    c = 1
+    while m % (2 * c) == 0 and m // (2 * c) >= rows:
+        c *= 2
+    return c
+
+
+def _linear(x: torch.Tensor, layer: nn.Linear) -> torch.Tensor:
+    if torch.is_grad_enabled() and x.dim() == 2 and x.shape[0] >= 65536:
+        return _SplitKLinear.apply(x, layer.weight, layer.bias)
+    return layer(x)
+
+
+def _trunk(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    for mod in seq:
+        x = _linear(x, mod) if isinstance(mod, nn.Linear) else mod(x)
+    return x
+
+
 def _mlp(in_dim: int, hidden=(128, 128)) -> nn.Sequential:
     layers, d = [], in_dim
     for h in hidden:
@@ -48,8 +95,8 @@ class ActorCritic(nn.Module):
                     nn.init.zeros_(m.bias)
 
     def forward_heads(self, obs: torch.Tensor):
-        mean = self.action_net(self.mlp_extractor.policy_net(obs))
-        value = self.value_net(self.mlp_extractor.value_net(obs)).squeeze(-1)
+        mean = _linear(_trunk(self.mlp_extractor.policy_net, obs), self.action_net)
+        value = _linear(_trunk(self.mlp_extractor.value_net, obs), self.value_net).squeeze(-1)
         return mean, value
 
     def value(self, obs: torch.Tensor) -> torch.Tensor:

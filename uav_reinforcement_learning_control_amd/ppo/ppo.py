@@ -105,7 +105,8 @@ class PPO:
         torch.manual_seed(seed)  # identical policy init on every rank
         self.policy = (policy or ActorCritic(12, 4, self.cfg.net_arch)).to(self.device)
         self.params = [p for p in self.policy.parameters()]
-        self.opt = torch.optim.Adam(self.params, lr=self.cfg.learning_rate, eps=self.cfg.adam_eps)
+        self.opt = torch.optim.Adam(self.params, lr=self.cfg.learning_rate, eps=self.cfg.adam_eps,
+                                    fused=self.device.type == "cuda")  # one kernel per step
         torch.manual_seed(seed + 1000 * (dist.get_rank() if self.world > 1 else 0))
         T, n = self.cfg.n_steps, env.num_envs
         f32 = dict(dtype=torch.float32, device=self.device)
