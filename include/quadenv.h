@@ -32,12 +32,17 @@
 extern "C" {
 #endif
 
-#define QUADENV_ABI_VERSION 1
+#define QUADENV_ABI_VERSION 2
 
 enum { QUAD_OK = 0, QUAD_EINVAL = -1, QUAD_EHIP = -2, QUAD_ENOMEM = -3, QUAD_EMODEL = -4 };
-enum { QUAD_ENV_HOVER = 0, QUAD_ENV_TRAJ = 1 };
+/* QUAD_ENV_BRAX_HOVER / QUAD_ENV_BRAX_TRAJ: the brax Env API siblings of the same path
+ * (train_brax_ppo.py QuadHoverBraxEnv :39-176 / JaxMJXQuadBraxEnv :179-368) as brax's ppo.train
+ * wraps them (EpisodeWrapper truncation, AutoResetWrapper restoring the episode's first state):
+ * 21-D raw obs [qpos(11), qvel(10)], clipped physical action -> mixer (no voltage), mjx.step
+ * semantics (no MuJoCo-C bad-state resets). */
+enum { QUAD_ENV_HOVER = 0, QUAD_ENV_TRAJ = 1, QUAD_ENV_BRAX_HOVER = 2, QUAD_ENV_BRAX_TRAJ = 3 };
 enum { QUAD_WRAP_NONE = 0, QUAD_WRAP_CTBR = 1 };
-enum { QUAD_NQ = 11, QUAD_NV = 10, QUAD_OBS = 12, QUAD_ACT = 4 };
+enum { QUAD_NQ = 11, QUAD_NV = 10, QUAD_OBS = 12, QUAD_OBS_BRAX = 21, QUAD_ACT = 4 };
 
 /* Env configuration. quad_default_cfg() fills the reference's defaults:
  *  HoverEnv.__init__ (hover_env.py:15-100), TrajectoryFollowEnv.__init__
@@ -57,6 +62,15 @@ typedef struct QuadCfg {
   double nominal_voltage, min_voltage, vdrop_base, vdrop_load;
   double rate_max_rad, rate_kd[3], rate_ki, rate_imax, inertia[3], max_torque;
   double timestep, gravity[3], density, viscosity;
+  /* brax kinds only (train_brax_ppo.py): target = target_low (QuadHoverBraxEnv (0,0,1));
+   * position limits = term_low/high[0..2] (|x|,|y| <= 3, z in [0.02, 4]); act_low/high = the
+   * clip range of the physical action; max_episode_steps = --episode-length (500). */
+  float reset_noise;            /* U(+-noise) on qpos and qvel at reset (0.01) */
+  float reward_pos_coef;        /* exp(-coef |pos - target|^2): 2 hover, 1 jax_mjx */
+  float reward_action_coef;     /* - coef |a|^2 (jax_mjx 0.001) */
+  float vel_limit;              /* jax_mjx: any |v_i| > limit invalidates (20) */
+  float traj_center[3], traj_amp[3], traj_freq[3];  /* jax_mjx sinusoid target */
+  float traj_duration;          /* seconds spanned by the episode_length samples (5) */
 } QuadCfg;
 
 /* Env state in field-major SoA: each array is [fields][N] (qpos [11][N], qvel [10][N], ...).
@@ -75,12 +89,13 @@ typedef struct QuadStateSoA {
 } QuadStateSoA;
 
 /* Outputs of quad_step (device pointers). Required: obs, reward, terminated, truncated.
- *  obs            [N,12] normalized observation (after auto-reset for envs that finished)
+ *  obs            [N,12] normalized observation (after auto-reset for envs that finished);
+ *                        brax kinds: [N,21] raw [qpos, qvel]
  *  reward         [N]    exp(-|pos - target|^2)           (hover_env.py:138-141)
  *  terminated     [N]    NaN / state-bounds termination   (hover_env.py:150-157)
  *  truncated      [N]    step_count >= max_episode_steps  (hover_env.py:188)
  * Optional (NULL to skip):
- *  terminal_obs   [N,12] obs before auto-reset (SB3 info["terminal_observation"]); only rows of
+ *  terminal_obs   [N,12|21] obs before auto-reset (SB3 info["terminal_observation"]); only rows of
  *                        envs that finished this step are written
  *  motor_commands [N,4]  info["motor_commands"] (N)
  *  voltage_scale  [N]    info["voltage_scale"]

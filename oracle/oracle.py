@@ -18,7 +18,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libquadoracle.so")
 
-ENV_HOVER, ENV_TRAJ = 0, 1
+ENV_HOVER, ENV_TRAJ, ENV_BRAX_HOVER, ENV_BRAX_TRAJ = 0, 1, 2, 3
 WRAP_NONE, WRAP_CTBR = 0, 1
 
 
@@ -58,6 +58,30 @@ class OracleStepOut(C.Structure):
                 ("voltage_scale", C.c_double), ("env_action", C.c_float * 4)]
 
 
+class OracleBraxCfg(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("episode_length", C.c_int32), ("target", C.c_float * 3),
+                ("pos_limit_xy", C.c_float), ("pos_limit_z_low", C.c_float),
+                ("pos_limit_z_high", C.c_float), ("vel_limit", C.c_float),
+                ("reset_noise", C.c_float), ("reward_pos_coef", C.c_float),
+                ("reward_action_coef", C.c_float), ("ctrl_min", C.c_float * 4),
+                ("ctrl_max", C.c_float * 4), ("traj_center", C.c_float * 3),
+                ("traj_amp", C.c_float * 3), ("traj_freq", C.c_float * 3),
+                ("traj_duration", C.c_float), ("max_motor_thrust", C.c_double),
+                ("arm_length", C.c_double), ("yaw_coeff", C.c_double), ("opt", OracleOpt)]
+
+
+class OracleBraxEnv(C.Structure):
+    _fields_ = [("qpos", C.c_double * 11), ("qvel", C.c_double * 10),
+                ("first_qpos", C.c_double * 11), ("first_qvel", C.c_double * 10),
+                ("steps", C.c_int32), ("env_steps", C.c_int32)]
+
+
+class OracleBraxOut(C.Structure):
+    _fields_ = [("obs", C.c_float * 21), ("terminal_obs", C.c_float * 21), ("reward", C.c_double),
+                ("terminated", C.c_int32), ("truncated", C.c_int32),
+                ("motor_commands", C.c_double * 4), ("target", C.c_float * 3)]
+
+
 _lib = None
 
 
@@ -93,8 +117,19 @@ def lib():
         L.oracle_random_action.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, fp]
         L.oracle_bench_rollout.argtypes = [C.POINTER(OracleCfg), C.c_int32, C.c_int32, C.c_uint64]
         L.oracle_bench_rollout.restype = C.c_double
-        for n in ("oracle_sizeof_env", "oracle_sizeof_stepout", "oracle_sizeof_cfg"):
+        L.oracle_mjx_step.argtypes = [C.POINTER(OracleOpt), dp, dp, dp]
+        L.oracle_brax_default_cfg.argtypes = [C.c_int32, C.POINTER(OracleBraxCfg)]
+        L.oracle_brax_reset_draw.argtypes = [C.POINTER(OracleBraxCfg), C.c_uint64, C.c_uint64,
+                                             C.c_uint32, fp]
+        L.oracle_brax_reset.argtypes = [C.POINTER(OracleBraxCfg), C.POINTER(OracleBraxEnv), fp, fp]
+        L.oracle_brax_step.argtypes = [C.POINTER(OracleBraxCfg), C.POINTER(OracleBraxEnv), fp,
+                                       C.c_int32, C.POINTER(OracleBraxOut)]
+        for n in ("oracle_sizeof_env", "oracle_sizeof_stepout", "oracle_sizeof_cfg",
+                  "oracle_sizeof_brax_cfg", "oracle_sizeof_brax_env", "oracle_sizeof_brax_out"):
             getattr(L, n).restype = C.c_size_t
+        assert L.oracle_sizeof_brax_cfg() == C.sizeof(OracleBraxCfg)
+        assert L.oracle_sizeof_brax_env() == C.sizeof(OracleBraxEnv)
+        assert L.oracle_sizeof_brax_out() == C.sizeof(OracleBraxOut)
         assert L.oracle_sizeof_env() == C.sizeof(OracleEnv)
         assert L.oracle_sizeof_stepout() == C.sizeof(OracleStepOut)
         assert L.oracle_sizeof_cfg() == C.sizeof(OracleCfg)
@@ -235,3 +270,33 @@ def out_to_dict(o: OracleStepOut) -> dict:
                 motor_commands=np.array(o.motor_commands[:], np.float64),
                 voltage=float(o.voltage), voltage_scale=float(o.voltage_scale),
                 env_action=np.array(o.env_action[:], np.float32))
+
+
+class BraxEnv:
+    """One brax-compat reference env (QuadHoverBraxEnv / JaxMJXQuadBraxEnv) under brax's
+    EpisodeWrapper + AutoResetWrapper (see oracle/brax_oracle.c)."""
+
+    def __init__(self, kind: int = ENV_BRAX_HOVER, episode_length: int = 500):
+        self.cfg = OracleBraxCfg()
+        lib().oracle_brax_default_cfg(kind, C.byref(self.cfg))
+        self.cfg.episode_length = int(episode_length)
+        self.s = OracleBraxEnv()
+
+    def draw(self, seed: int, gid: int, episode: int):
+        u = np.zeros(21, np.float32)
+        lib().oracle_brax_reset_draw(C.byref(self.cfg), seed, gid, episode, _fp(u))
+        return u
+
+    def reset_with(self, u21):
+        u = np.ascontiguousarray(u21, dtype=np.float32)
+        obs = np.zeros(21, np.float32)
+        lib().oracle_brax_reset(C.byref(self.cfg), C.byref(self.s), _fp(u), _fp(obs))
+        return obs
+
+    def step(self, action, auto_reset: bool = True) -> dict:
+        a = np.ascontiguousarray(action, dtype=np.float32)
+        o = OracleBraxOut()
+        lib().oracle_brax_step(C.byref(self.cfg), C.byref(self.s), _fp(a), int(auto_reset), C.byref(o))
+        return dict(obs=np.array(o.obs[:], np.float32), terminal_obs=np.array(o.terminal_obs[:], np.float32),
+                    reward=float(o.reward), terminated=bool(o.terminated), truncated=bool(o.truncated),
+                    motor_commands=np.array(o.motor_commands[:]), target=np.array(o.target[:], np.float32))

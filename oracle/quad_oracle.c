@@ -452,6 +452,21 @@ static void reset_data(double* qpos, double* qvel, double* ctrl) { /* mj_resetDa
   memset(ctrl, 0, 4 * sizeof(double));
 }
 
+/* mj_Euler (no dof damping) -> mj_advance: semi-implicit Euler */
+static void euler_advance(const OracleOpt* opt, double* qpos, double* qvel, const double* qacc) {
+  const double h = opt->timestep;
+  for (int i = 0; i < NV; i++) qvel[i] += h * qacc[i];
+  for (int i = 0; i < 3; i++) qpos[i] += h * qvel[i];
+  { /* mju_quatIntegrate(qpos+3, qvel+3, h) */
+    double ax[3] = {qvel[3], qvel[4], qvel[5]}, qrot[4];
+    const double angle = h * normalize3(ax);
+    axisangle2quat(qrot, ax, angle);
+    normalize4(qpos + 3);
+    mulquat(qpos + 3, qpos + 3, qrot);
+  }
+  for (int i = 0; i < 4; i++) qpos[7 + i] += h * qvel[6 + i];
+}
+
 int oracle_mj_step(const OracleOpt* opt, double* qpos, double* qvel, double* ctrl) {
   int warn = 0;
   for (int i = 0; i < ORACLE_NQ; i++)
@@ -476,19 +491,21 @@ int oracle_mj_step(const OracleOpt* opt, double* qpos, double* qvel, double* ctr
       warn |= 8;
       break;
     }
-  /* mj_Euler (no dof damping) -> mj_advance: semi-implicit Euler */
-  const double h = opt->timestep;
-  for (int i = 0; i < NV; i++) qvel[i] += h * qacc[i];
-  for (int i = 0; i < 3; i++) qpos[i] += h * qvel[i];
-  { /* mju_quatIntegrate(qpos+3, qvel+3, h) */
-    double ax[3] = {qvel[3], qvel[4], qvel[5]}, qrot[4];
-    const double angle = h * normalize3(ax);
-    axisangle2quat(qrot, ax, angle);
-    normalize4(qpos + 3);
-    mulquat(qpos + 3, qpos + 3, qrot);
-  }
-  for (int i = 0; i < 4; i++) qpos[7 + i] += h * qvel[6 + i];
+  euler_advance(opt, qpos, qvel, qacc);
   return warn;
+}
+
+/* mjx.step: the same forward dynamics and Euler step without MuJoCo C's bad-state checks
+ * (MJX raises no warnings: a NaN/huge state or ctrl propagates; jnp.clip keeps NaN). */
+void oracle_mjx_step(const OracleOpt* opt, double* qpos, double* qvel, const double* ctrl) {
+  double c[4];
+  for (int i = 0; i < 4; i++) {
+    c[i] = ctrl[i];
+    if (c[i] < ctrl_lo) c[i] = ctrl_lo; else if (c[i] > ctrl_hi) c[i] = ctrl_hi;
+  }
+  double M[NV][NV], bias[NV], passive[NV], actf[NV], qacc[NV];
+  forward_full(opt, qpos, qvel, c, M, bias, passive, actf, qacc);
+  euler_advance(opt, qpos, qvel, qacc);
 }
 
 /* ---------------------------------------------------------------------------------------

@@ -146,3 +146,27 @@ def test_euler_matches_scipy_directly():
         q = rng.normal(size=4)
         e = O.quat_to_euler(q)
         np.testing.assert_allclose(e, R.from_quat([q[1], q[2], q[3], q[0]]).as_euler("xyz"), atol=1e-13)
+
+
+def test_brax_oracle_reset_draw_and_free_fall():
+    """brax kinds (oracle/brax_oracle.c): reset noise within +-0.01 with the jax_mjx quaternion
+    renormalized; from rest at z = 1 with zero motor force (thrust 0, torques 0 -> a = (-1, 0, 0, 0)),
+    one step is one semi-implicit Euler step of free fall (drag is zero at rest)."""
+    import numpy as np
+    from oracle import oracle as O
+    for kind in (O.ENV_BRAX_HOVER, O.ENV_BRAX_TRAJ):
+        e = O.BraxEnv(kind)
+        u = e.draw(3, 17, 0)
+        assert np.all(np.abs(u) <= 0.01) and np.unique(u).size == 21
+        obs = e.reset_with(u)
+        if kind == O.ENV_BRAX_TRAJ:
+            assert abs(np.linalg.norm(obs[3:7]) - 1.0) < 1e-6 and abs(obs[2] - 1.0) < 0.011
+        else:
+            assert np.array_equal(obs[:11], (np.array([0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0], np.float32) + u[:11]))
+    e = O.BraxEnv(O.ENV_BRAX_TRAJ)
+    obs = e.reset_with(np.zeros(21, np.float32))
+    r = e.step(np.array([-1.0, 0.0, 0.0, 0.0], np.float32))
+    assert np.allclose(r["motor_commands"], 0.0)
+    assert abs(r["obs"][13] - (-9.81 * 0.01)) < 1e-9       # v_z
+    assert abs(r["obs"][2] - (1.0 - 9.81 * 0.01 * 0.01)) < 1e-7  # z
+    assert not r["terminated"] and not r["truncated"]

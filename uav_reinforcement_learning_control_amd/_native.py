@@ -13,9 +13,9 @@ LIB_PATH = os.path.join(_PKG, "_lib", "libquadenv.so")
 CSRC = os.path.join(_PKG, "csrc")
 
 QUAD_OK, QUAD_EINVAL, QUAD_EHIP, QUAD_ENOMEM, QUAD_EMODEL = 0, -1, -2, -3, -4
-ENV_HOVER, ENV_TRAJ = 0, 1
+ENV_HOVER, ENV_TRAJ, ENV_BRAX_HOVER, ENV_BRAX_TRAJ = 0, 1, 2, 3
 WRAP_NONE, WRAP_CTBR = 0, 1
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class QuadCfg(C.Structure):
@@ -34,6 +34,10 @@ class QuadCfg(C.Structure):
         ("rate_imax", C.c_double), ("inertia", C.c_double * 3), ("max_torque", C.c_double),
         ("timestep", C.c_double), ("gravity", C.c_double * 3), ("density", C.c_double),
         ("viscosity", C.c_double),
+        ("reset_noise", C.c_float), ("reward_pos_coef", C.c_float),
+        ("reward_action_coef", C.c_float), ("vel_limit", C.c_float),
+        ("traj_center", C.c_float * 3), ("traj_amp", C.c_float * 3), ("traj_freq", C.c_float * 3),
+        ("traj_duration", C.c_float),
     ]
 
 

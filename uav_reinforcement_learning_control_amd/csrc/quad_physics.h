@@ -166,6 +166,10 @@ struct KConsts {
   double rate_max, rate_ikd[3], rate_kidt, rate_imax, max_torque;
   double r_vnom, r_mx, r_max_torque;  // reciprocals (1-ulp float64 differences, far below 1e-12)
   int32_t max_steps;
+  // brax kinds (float32 like the JAX reference)
+  float bx_noise, bx_rpos, bx_ract, bx_vlim;
+  float bx_tc[3], bx_ta[3], bx_tw[3];  // sinusoid center, amplitude, 2 pi f (float32 products)
+  float bx_tdt, bx_tdur;               // linspace step dur / (L - 1), dur
 };
 
 template <typename T>
@@ -215,6 +219,17 @@ inline void make_kconsts(const QuadCfg& cfg, const PhysConstsD& d, KConsts<T>& k
   k.r_mx = 1.0 / (cfg.max_motor_thrust > 1e-6 ? cfg.max_motor_thrust : 1e-6);
   k.r_max_torque = 1.0 / cfg.max_torque;
   k.max_steps = cfg.max_episode_steps;
+  k.bx_noise = cfg.reset_noise;
+  k.bx_rpos = cfg.reward_pos_coef;
+  k.bx_ract = cfg.reward_action_coef;
+  k.bx_vlim = cfg.vel_limit;
+  for (int i = 0; i < 3; i++) {
+    k.bx_tc[i] = cfg.traj_center[i];
+    k.bx_ta[i] = cfg.traj_amp[i];
+    k.bx_tw[i] = float(2.0f * float(M_PI)) * cfg.traj_freq[i];  // (2.0 * jp.pi) * freq, float32
+  }
+  k.bx_tdur = cfg.traj_duration;
+  k.bx_tdt = cfg.max_episode_steps > 1 ? cfg.traj_duration / float(cfg.max_episode_steps - 1) : 0.f;
 }
 
 // Per-env state held in registers for one step.
@@ -360,7 +375,9 @@ QD_HD void normalize4(T q[4]) {
 }
 
 // mujoco.mj_step for one env. Fin: ctrl in float64 (may be NaN / out of range; MuJoCo semantics).
-template <typename T>
+// CHECKS = false: mjx.step semantics (the brax kinds): no bad-state / bad-ctrl / bad-acc resets,
+// NaN propagates.
+template <typename T, bool CHECKS = true>
 QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4]) {
   // mj_checkPos / mj_checkVel: bad state => mj_resetData (qpos0, zero qvel, zero ctrl)
   bool bad = false;
@@ -371,6 +388,7 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
   bool badctrl = false;
 #pragma unroll
   for (int i = 0; i < 4; i++) badctrl |= isbad(Fin[i]);
+  if (!CHECKS) bad = badctrl = false;
   if (bad) {
 #pragma unroll
     for (int i = 0; i < 3; i++) { e.pos[i] = T(0); e.v[i] = T(0); e.w[i] = T(0); }
@@ -399,7 +417,7 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
   for (int i = 0; i < 3; i++) badacc |= int(isbad(vdot[i])) | int(isbad(wdot[i]));
 #pragma unroll
   for (int i = 0; i < 4; i++) badacc |= isbad(sdot[i]);
-  if (badacc) {  // mj_checkAcc: reset to qpos0 with zero ctrl; at rest there the only force is
+  if (CHECKS && badacc) {  // mj_checkAcc: reset to qpos0 with zero ctrl; at rest there the only force is
                  // gravity, so qacc = (0, 0, gz, 0, ...) exactly (cf. oracle K1)
 #pragma unroll
     for (int i = 0; i < 3; i++) { e.pos[i] = T(0); e.v[i] = T(0); e.w[i] = T(0); vdot[i] = T(0); wdot[i] = T(0); }
@@ -664,6 +682,139 @@ QD_HD void env_reset_from(const KConsts<T>& k, EnvRegs<T>& e, const float init12
     const float x = i < 3 ? sub32(e.target[i], s12[i]) : s12[i];
     obs[i] = norm_obs1(x, k.obs_lo[i], k.obs_span[i], k.obs_rspan[i]);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// brax kinds (train_brax_ppo.py). Step: QuadHoverBraxEnv.step (:131-173) / JaxMJXQuadBraxEnv.step
+// (:300-356) for one env; obs21 = [qpos, qvel] (:175-176, :365-366). `term` = the env's done.
+template <typename T, int KIND>
+QD_HD void brax_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], float obs21[21],
+                     float& reward, bool& term, bool& trunc, float motor[4]) {
+  // (action + 1) * 0.5 * (max - min) + min, clipped (float32 elementwise like JAX, no FMA
+  // contraction; jnp.clip keeps NaN). The mixer then runs in float64: four ~13 N motor forces
+  // cancel to mN*m torques, where float32 rounding alone would exceed the 1e-5 parity bar.
+  float u[4];
+  {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const float lo = k.act_lo[j], hi = lo + k.act_span[j];
+      const float p = (act[j] + 1.0f) * 0.5f * k.act_span[j] + lo;
+      u[j] = p < lo ? lo : (p > hi ? hi : p);
+    }
+  }
+  double F[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double s = k.ph.mix[4 * i] * double(u[0]) + k.ph.mix[4 * i + 1] * double(u[1]) +
+                     k.ph.mix[4 * i + 2] * double(u[2]) + k.ph.mix[4 * i + 3] * double(u[3]);
+    F[i] = s < 0.0 ? 0.0 : (s > k.max_thrust ? k.max_thrust : s);
+    motor[i] = float(F[i]);
+  }
+  physics_step<T, false>(k.ph, e, F);
+  e.step += 1;
+  const float pos[3] = {float(e.pos[0]), float(e.pos[1]), float(e.pos[2])};
+  float tgt[3] = {e.target[0], e.target[1], e.target[2]};
+  if (KIND == QUAD_ENV_BRAX_TRAJ) {
+    // info["step_count"] lives in rint[0] (a float counter; brax's AutoResetWrapper never resets it)
+    const float cnt = float(e.rint[0]) + 1.0f;
+    e.rint[0] = T(cnt);
+    const float lastf = float(k.max_steps - 1);
+    const float idx = cnt < lastf ? cnt : lastf;
+    const float t = idx == lastf ? k.bx_tdur : idx * k.bx_tdt;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      float sn, cs;
+      q_sincos(k.bx_tw[i] * t, &sn, &cs);
+      tgt[i] = k.bx_tc[i] + k.bx_ta[i] * sn;
+      e.target[i] = tgt[i];
+    }
+  }
+  obs21[0] = pos[0]; obs21[1] = pos[1]; obs21[2] = pos[2];
+#pragma unroll
+  for (int i = 0; i < 4; i++) { obs21[3 + i] = float(e.q[i]); obs21[7 + i] = float(e.th[i]); }
+#pragma unroll
+  for (int i = 0; i < 3; i++) { obs21[11 + i] = float(e.v[i]); obs21[14 + i] = float(e.w[i]); }
+#pragma unroll
+  for (int i = 0; i < 4; i++) obs21[17 + i] = float(e.s[i]);
+  float d2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 3; i++) { const float d = pos[i] - tgt[i]; d2 += d * d; }
+  const float per = fsqrt(d2);
+  const bool oxy = q_abs(pos[0]) > k.term_hi[0] || q_abs(pos[1]) > k.term_hi[1];
+  const bool oz = pos[2] < k.term_lo[2] || pos[2] > k.term_hi[2];
+  if (KIND == QUAD_ENV_BRAX_TRAJ) {
+    bool fin = true;
+#pragma unroll
+    for (int i = 0; i < 21; i++) fin &= q_abs(obs21[i]) <= 3.4028235e38f;  // isfinite (NaN fails)
+    bool ov = false;
+#pragma unroll
+    for (int i = 0; i < 3; i++) ov |= q_abs(obs21[11 + i]) > k.bx_vlim;
+    const bool valid = fin && !oxy && !oz && !ov;
+    const float pe = (valid && q_abs(per) <= 3.4028235e38f) ? per : 1e3f;
+    float asq = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) asq += act[j] * act[j];
+    const float rr = q_exp(-k.bx_rpos * pe * pe) - k.bx_ract * asq;
+    reward = (valid && q_abs(rr) <= 3.4028235e38f) ? rr : -1.0f;
+    term = !valid;
+#pragma unroll
+    for (int i = 0; i < 21; i++) obs21[i] = q_abs(obs21[i]) <= 3.4028235e38f ? obs21[i] : 0.f;
+  } else {
+    reward = q_exp(-k.bx_rpos * per * per);
+    term = oxy || oz;  // NaN compares false: QuadHoverBraxEnv has no NaN guard
+  }
+  trunc = e.step >= k.max_steps;  // EpisodeWrapper
+}
+
+// brax reset draw: 21 x U(-noise, noise) from Philox(seed; gid, episode, 0x300 + block)
+QD_HD void brax_reset_draw(float noise, uint64_t seed, uint64_t gid, uint32_t episode, float u21[21]) {
+  uint32_t r[24];
+#pragma unroll
+  for (uint32_t blk = 0; blk < 6; blk++) {
+    uint32_t c[4] = {uint32_t(gid), uint32_t(gid >> 32), episode, 0x300u + blk};
+    philox4x32_10(c, uint32_t(seed), uint32_t(seed >> 32));
+    r[4 * blk] = c[0]; r[4 * blk + 1] = c[1]; r[4 * blk + 2] = c[2]; r[4 * blk + 3] = c[3];
+  }
+#pragma unroll
+  for (int i = 0; i < 21; i++) u21[i] = affine32(-noise, u01(r[i]), 2.0f * noise);
+}
+
+// QuadHoverBraxEnv.reset (:102-129) / JaxMJXQuadBraxEnv.reset (:255-294) from the draw.
+// keep_counter: AutoResetWrapper restore (the env's step_count carries on).
+template <typename T, int KIND>
+QD_HD void brax_reset_from(const KConsts<T>& k, EnvRegs<T>& e, const float u21[21], float obs21[21],
+                           bool keep_counter) {
+  const float z0 = KIND == QUAD_ENV_BRAX_TRAJ ? 1.0f : 0.0f;
+  float q[11] = {0.f, 0.f, z0, 1.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 11; i++) q[i] = q[i] + u21[i];
+  if (KIND == QUAD_ENV_BRAX_TRAJ) {
+    const float n = fsqrt(q[3] * q[3] + q[4] * q[4] + q[5] * q[5] + q[6] * q[6]) + 1e-8f;
+#pragma unroll
+    for (int i = 3; i < 7; i++) q[i] = q[i] / n;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    e.pos[i] = T(q[i]);
+    e.v[i] = T(u21[11 + i]);
+    e.w[i] = T(u21[14 + i]);
+    e.target[i] = KIND == QUAD_ENV_BRAX_HOVER ? k.tgt_lo[i] : k.bx_tc[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    e.q[i] = T(q[3 + i]);
+    e.th[i] = T(q[7 + i]);
+    e.s[i] = T(u21[17 + i]);
+  }
+  e.volt = T(0);
+  if (!keep_counter) { e.rint[0] = T(0); }
+  e.rint[1] = e.rint[2] = T(0);
+  e.step = 0;
+#pragma unroll
+  for (int i = 0; i < 11; i++) obs21[i] = q[i];
+#pragma unroll
+  for (int i = 0; i < 10; i++) obs21[11 + i] = u21[11 + i];
 }
 
 }  // namespace quadenv

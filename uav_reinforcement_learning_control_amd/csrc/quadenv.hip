@@ -633,6 +633,69 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KParams p, const uint8_t* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// brax kinds: one thread per env (obs rows are 84 B, written directly). Auto-reset follows brax's
+// AutoResetWrapper: the env returns to the FIRST state of its episode -- regenerated from the draw
+// of the last explicit reset (episode counter - 1) instead of being stored.
+template <int KIND>
+__global__ __launch_bounds__(BLOCK) void k_step_brax(KParams p, const float4* __restrict__ act,
+                                                     QuadStepOut out) {
+  const int i = p.first + blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= p.first + p.count) return;
+  EnvRegs<float> e;
+  load_env(p, i, e, true);
+  const float4 a4 = act[i];
+  const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+  float obs[21], reward, motor[4];
+  bool term, trunc;
+  brax_step<float, KIND>(p.k, e, a, obs, reward, term, trunc, motor);
+  out.reward[i] = reward;
+  out.terminated[i] = term;
+  out.truncated[i] = trunc;
+  if (out.motor_commands)
+    reinterpret_cast<float4*>(out.motor_commands)[i] = make_float4(motor[0], motor[1], motor[2], motor[3]);
+  if (out.voltage_scale) out.voltage_scale[i] = 1.0f;
+  if ((term || trunc) && p.auto_reset) {
+    if (out.terminal_obs) {
+#pragma unroll
+      for (int j = 0; j < 21; j++) out.terminal_obs[size_t(i) * 21 + j] = obs[j];
+    }
+    float u21[21];
+    brax_reset_draw(p.k.bx_noise, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, u21);
+    brax_reset_from<float, KIND>(p.k, e, u21, obs, true);
+  }
+  store_env(p, i, e, true);
+#pragma unroll
+  for (int j = 0; j < 21; j++) out.obs[size_t(i) * 21 + j] = obs[j];
+}
+
+template <int KIND>
+__global__ __launch_bounds__(BLOCK) void k_reset_brax(KParams p, const uint8_t* __restrict__ mask,
+                                                      float* __restrict__ obs_out) {
+  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= p.n) return;
+  if (mask && !mask[i]) return;
+  const uint32_t ep = p.ep[i];
+  float u21[21], obs[21];
+  brax_reset_draw(p.k.bx_noise, p.seed, p.gid_base + uint64_t(i), ep, u21);
+  EnvRegs<float> e;
+  brax_reset_from<float, KIND>(p.k, e, u21, obs, false);
+  p.ep[i] = ep + 1u;
+  store_env(p, i, e, true);
+  if (obs_out) {
+#pragma unroll
+    for (int j = 0; j < 21; j++) obs_out[size_t(i) * 21 + j] = obs[j];
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_observe_brax(KParams p, float* __restrict__ obs_out) {
+  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= p.n) return;
+  const float* s = p.soa;
+#pragma unroll
+  for (int j = 0; j < 21; j++) obs_out[size_t(i) * 21 + j] = s[(F_QPOS + j) * p.n + i];  // qpos, qvel
+}
+
 __global__ __launch_bounds__(BLOCK) void k_observe(KParams p, float* __restrict__ obs_out,
                                                    float* __restrict__ s12_out) {
   const int i = blockIdx.x * BLOCK + threadIdx.x;
@@ -723,9 +786,11 @@ const char* quad_last_error(void) { return g_err.c_str(); }
 
 int quad_default_cfg(int32_t env_kind, int32_t wrapper, QuadCfg* c) {
   if (!c) return fail(QUAD_EINVAL, "cfg is NULL");
-  if (env_kind != QUAD_ENV_HOVER && env_kind != QUAD_ENV_TRAJ)
+  if (env_kind < QUAD_ENV_HOVER || env_kind > QUAD_ENV_BRAX_TRAJ)
     return fail(QUAD_EINVAL, "unknown env_kind");
   if (wrapper != QUAD_WRAP_NONE && wrapper != QUAD_WRAP_CTBR) return fail(QUAD_EINVAL, "unknown wrapper");
+  if (env_kind >= QUAD_ENV_BRAX_HOVER && wrapper != QUAD_WRAP_NONE)
+    return fail(QUAD_EINVAL, "the brax env kinds take no wrapper");
   std::memset(c, 0, sizeof *c);
   c->env_kind = env_kind;
   c->wrapper = wrapper;
@@ -769,6 +834,20 @@ int quad_default_cfg(int32_t env_kind, int32_t wrapper, QuadCfg* c) {
   c->gravity[2] = -9.81;
   c->density = 1.225;
   c->viscosity = 1.8e-5;
+  if (env_kind >= QUAD_ENV_BRAX_HOVER) {  // train_brax_ppo.py
+    const bool traj = env_kind == QUAD_ENV_BRAX_TRAJ;
+    c->max_episode_steps = 500;                        // --episode-length (:436)
+    for (int i = 0; i < 3; i++) { c->target_low[i] = c->target_high[i] = i == 2 ? 1.f : 0.f; }  // (:55)
+    c->term_low[0] = c->term_low[1] = -3.f; c->term_high[0] = c->term_high[1] = 3.f;  // (:48-50)
+    c->term_low[2] = 0.02f; c->term_high[2] = 4.f;
+    c->reset_noise = 0.01f;                            // (:105-116, :271-272)
+    c->reward_pos_coef = traj ? 1.f : 2.f;             // (:146 / :338)
+    c->reward_action_coef = traj ? 0.001f : 0.f;       // (:339)
+    c->vel_limit = traj ? 20.f : 0.f;                  // (:190)
+    const float cen[3] = {0.f, 0.f, 1.f}, amp[3] = {0.5f, 0.5f, 0.2f}, fr[3] = {0.2f, 0.15f, 0.1f};
+    for (int i = 0; i < 3; i++) { c->traj_center[i] = cen[i]; c->traj_amp[i] = amp[i]; c->traj_freq[i] = fr[i]; }
+    c->traj_duration = 5.f;                            // --traj-duration-seconds (:444)
+  }
   return QUAD_OK;
 }
 
@@ -779,10 +858,12 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   if (n_envs <= 0) return fail(QUAD_EINVAL, "n_envs must be > 0");
   if (int64_t(n_envs) * NF > int64_t(INT32_MAX) || int64_t(n_envs) * 4 > int64_t(INT32_MAX))
     return fail(QUAD_EINVAL, "n_envs too large");
-  if (cfg->env_kind != QUAD_ENV_HOVER && cfg->env_kind != QUAD_ENV_TRAJ)
+  if (cfg->env_kind < QUAD_ENV_HOVER || cfg->env_kind > QUAD_ENV_BRAX_TRAJ)
     return fail(QUAD_EINVAL, "unknown env_kind");
   if (cfg->wrapper != QUAD_WRAP_NONE && cfg->wrapper != QUAD_WRAP_CTBR)
     return fail(QUAD_EINVAL, "unknown wrapper");
+  if (cfg->env_kind >= QUAD_ENV_BRAX_HOVER && cfg->wrapper != QUAD_WRAP_NONE)
+    return fail(QUAD_EINVAL, "the brax env kinds take no wrapper");
   if (cfg->max_episode_steps <= 0) return fail(QUAD_EINVAL, "max_episode_steps must be > 0");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
@@ -853,7 +934,11 @@ int quad_reset(QuadHandle* h, const uint8_t* mask, float* obs, void* stream) {
   if (!h) return fail(QUAD_EINVAL, "handle is NULL");
   DeviceGuard g(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  if (h->cfg.env_kind == QUAD_ENV_TRAJ)
+  if (h->cfg.env_kind == QUAD_ENV_BRAX_HOVER)
+    hipLaunchKernelGGL(k_reset_brax<QUAD_ENV_BRAX_HOVER>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
+  else if (h->cfg.env_kind == QUAD_ENV_BRAX_TRAJ)
+    hipLaunchKernelGGL(k_reset_brax<QUAD_ENV_BRAX_TRAJ>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
+  else if (h->cfg.env_kind == QUAD_ENV_TRAJ)
     hipLaunchKernelGGL(k_reset<QUAD_ENV_TRAJ>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
   else
     hipLaunchKernelGGL(k_reset<QUAD_ENV_HOVER>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
@@ -886,7 +971,13 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
   KParams kp = h->kp;
   kp.first = first;
   kp.count = count;
-  if (G == 0) {  // legacy one-thread-per-env form with the LDS obs transpose (A/B reference)
+  if (h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) {
+    const dim3 grid(grid_of(count));
+    if (h->cfg.env_kind == QUAD_ENV_BRAX_TRAJ)
+      hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_TRAJ>), grid, blk, 0, s, kp, a, *out);
+    else
+      hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_HOVER>), grid, blk, 0, s, kp, a, *out);
+  } else if (G == 0) {  // legacy one-thread-per-env form with the LDS obs transpose (A/B reference)
     const dim3 grid(grid_of(count));
     if (traj && ctbr)
       hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, kp, a, *out);
@@ -917,6 +1008,13 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
 int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream) {
   if (!h || !obs) return fail(QUAD_EINVAL, "handle/obs is NULL");
   DeviceGuard g(h->device);
+  if (h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) {  // raw [qpos, qvel]; no QuadState
+    if (state12) return fail(QUAD_EINVAL, "state12 is not defined for the brax env kinds");
+    hipLaunchKernelGGL(k_observe_brax, dim3(grid_of(h->n)), dim3(BLOCK), 0,
+                       static_cast<hipStream_t>(stream), h->kp, obs);
+    HIP_TRY(hipGetLastError());
+    return QUAD_OK;
+  }
   hipLaunchKernelGGL(k_observe, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
                      h->kp, obs, state12);
   HIP_TRY(hipGetLastError());

@@ -4,6 +4,9 @@ Mirrors the reference's hot path and the vectorized interface its learners drive
   * HoverEnv.reset / step                 envs/hover_env.py:200-238, :159-198
   * RateControlWrapper (wrapper="RateControlWrapper")       envs/rate_wrapper.py:26-111
   * TrajectoryFollowEnv (env="trajectory")                  envs/trajectory_follow_env.py:14-253
+  * brax-compat kinds (env="brax_hover" QuadHoverBraxEnv, env="brax_jax_mjx" JaxMJXQuadBraxEnv,
+    train_brax_ppo.py:39-368): 21-D raw obs; auto-reset restores the episode's first state
+    (brax AutoResetWrapper); the functional brax API sits on top in envs/brax_env.py
   * SB3 VecEnv auto-reset (make_vec_env, train.py:48): on terminated|truncated the returned
     obs is the reset obs, info["terminal_observation"] the final one and
     info["TimeLimit.truncated"] = truncated & ~terminated.
@@ -24,7 +27,10 @@ from .. import _native as N
 from ..utils.spaces import Box
 
 _ENV_KINDS = {"hover": N.ENV_HOVER, "HoverEnv": N.ENV_HOVER,
-              "trajectory": N.ENV_TRAJ, "TrajectoryFollowEnv": N.ENV_TRAJ}
+              "trajectory": N.ENV_TRAJ, "TrajectoryFollowEnv": N.ENV_TRAJ,
+              "brax_hover": N.ENV_BRAX_HOVER, "QuadHoverBraxEnv": N.ENV_BRAX_HOVER,
+              "brax_jax_mjx": N.ENV_BRAX_TRAJ, "jax_mjx_quad": N.ENV_BRAX_TRAJ,
+              "JaxMJXQuadBraxEnv": N.ENV_BRAX_TRAJ}
 _WRAPPERS = {None: N.WRAP_NONE, "none": N.WRAP_NONE, "RateControlWrapper": N.WRAP_CTBR,
              "ctbr": N.WRAP_CTBR}
 
@@ -75,14 +81,17 @@ class QuadVecEnv:
                               self.num_envs, C.byref(h)), "quad_create")
         self._h = h
         self.action_space = Box(-1.0, 1.0, (4,), np.float32)
-        self.observation_space = Box(-1.0, 1.0, (12,), np.float32)
+        self.brax = cfg.env_kind >= N.ENV_BRAX_HOVER
+        self.obs_dim = 21 if self.brax else 12
+        self.observation_space = (Box(-np.inf, np.inf, (21,), np.float32) if self.brax
+                                  else Box(-1.0, 1.0, (12,), np.float32))
         n, dev = self.num_envs, self.device
         f32 = dict(dtype=torch.float32, device=dev)
-        self.obs = torch.zeros(n, 12, **f32)
+        self.obs = torch.zeros(n, self.obs_dim, **f32)
         self.reward = torch.zeros(n, **f32)
         self.terminated = torch.zeros(n, dtype=torch.bool, device=dev)
         self.truncated = torch.zeros(n, dtype=torch.bool, device=dev)
-        self.terminal_obs = torch.zeros(n, 12, **f32)
+        self.terminal_obs = torch.zeros(n, self.obs_dim, **f32)
         self.motor_commands = torch.zeros(n, 4, **f32)
         self.voltage_scale = torch.zeros(n, **f32)
         self.state12 = torch.zeros(n, 12, **f32)
@@ -113,11 +122,12 @@ class QuadVecEnv:
 
     def reset(self, seed: Optional[int] = None, mask: Optional[torch.Tensor] = None,
               out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """HoverEnv.reset for all envs (or those with mask != 0); returns obs [N,12]."""
+        """HoverEnv.reset for all envs (or those with mask != 0); returns obs [N,12] ([N,21] for
+        the brax kinds)."""
         if seed is not None:
             self.seed(seed)
         out = self.obs if out is None else out
-        self._check(out, (self.num_envs, 12), torch.float32)
+        self._check(out, (self.num_envs, self.obs_dim), torch.float32)
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
@@ -138,7 +148,7 @@ class QuadVecEnv:
         self._check(actions, (self.num_envs, 4), torch.float32)
         obs = self.obs if obs is None else obs
         reward = self.reward if reward is None else reward
-        self._check(obs, (self.num_envs, 12), torch.float32)
+        self._check(obs, (self.num_envs, self.obs_dim), torch.float32)
         self._check(reward, (self.num_envs,), torch.float32)
         full = info == "full"
         o = N.QuadStepOut(
@@ -147,7 +157,7 @@ class QuadVecEnv:
             terminal_obs=self.terminal_obs.data_ptr(),
             motor_commands=self.motor_commands.data_ptr() if full else None,
             voltage_scale=self.voltage_scale.data_ptr() if full else None,
-            state12=self.state12.data_ptr() if full else None)
+            state12=self.state12.data_ptr() if full and not self.brax else None)
         N.check(N.lib().quad_step(self._h, C.c_void_p(actions.data_ptr()), C.byref(o),
                                   self._stream()), "quad_step")
         inf = {"terminal_observation": self.terminal_obs}
@@ -162,7 +172,9 @@ class QuadVecEnv:
         """HoverEnv._get_obs of the current state; with state=True also the absolute 12-D
         QuadState vector (returns (obs, state12))."""
         out = self.obs if out is None else out
-        self._check(out, (self.num_envs, 12), torch.float32)
+        self._check(out, (self.num_envs, self.obs_dim), torch.float32)
+        if state and self.brax:
+            raise ValueError("state=True: the brax kinds have no QuadState (obs is the raw state)")
         N.check(N.lib().quad_observe(self._h, _ptr(out), _ptr(self.state12) if state else None,
                                      self._stream()), "quad_observe")
         return (out, self.state12) if state else out
