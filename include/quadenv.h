@@ -41,8 +41,10 @@ enum { QUAD_OK = 0, QUAD_EINVAL = -1, QUAD_EHIP = -2, QUAD_ENOMEM = -3, QUAD_EMO
  * 21-D raw obs [qpos(11), qvel(10)], clipped physical action -> mixer (no voltage), mjx.step
  * semantics (no MuJoCo-C bad-state resets). */
 enum { QUAD_ENV_HOVER = 0, QUAD_ENV_TRAJ = 1, QUAD_ENV_BRAX_HOVER = 2, QUAD_ENV_BRAX_TRAJ = 3 };
-enum { QUAD_WRAP_NONE = 0, QUAD_WRAP_CTBR = 1 };
-enum { QUAD_NQ = 11, QUAD_NV = 10, QUAD_OBS = 12, QUAD_OBS_BRAX = 21, QUAD_ACT = 4 };
+/* QUAD_WRAP_RELPOS: RelPosActWrapper (envs/wrappers.py:13-25): 7-D obs [normalized rel pos (3),
+ * previous action (4)] of the hover / trajectory kinds (quad_step's obs is then [N,7]). */
+enum { QUAD_WRAP_NONE = 0, QUAD_WRAP_CTBR = 1, QUAD_WRAP_RELPOS = 2 };
+enum { QUAD_NQ = 11, QUAD_NV = 10, QUAD_OBS = 12, QUAD_OBS_BRAX = 21, QUAD_OBS_RELPOS = 7, QUAD_ACT = 4 };
 
 /* Env configuration. quad_default_cfg() fills the reference's defaults:
  *  HoverEnv.__init__ (hover_env.py:15-100), TrajectoryFollowEnv.__init__
@@ -77,7 +79,8 @@ typedef struct QuadCfg {
  * qpos = MuJoCo qpos (x y z qw qx qy qz theta1..4), qvel = MuJoCo qvel (world v, body omega,
  * prop rates); voltage = HoverEnv.voltage; target = target_state.position; rate_int =
  * RateControlWrapper._rate_int_torque; step_count = HoverEnv._step_count; episode = the number of
- * resets drawn so far (the reset RNG counter). NULL members are skipped by get/set. */
+ * resets drawn so far (the reset RNG counter); prev_action = HoverEnv._prev_action [4][N] (kept for
+ * QUAD_WRAP_RELPOS). NULL members are skipped by get/set. */
 typedef struct QuadStateSoA {
   float* qpos;
   float* qvel;
@@ -86,6 +89,7 @@ typedef struct QuadStateSoA {
   float* rate_int;
   int32_t* step_count;
   uint32_t* episode;
+  float* prev_action;
 } QuadStateSoA;
 
 /* Outputs of quad_step (device pointers). Required: obs, reward, terminated, truncated.

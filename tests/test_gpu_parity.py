@@ -322,3 +322,35 @@ def test_step_range_touches_only_its_rows(kernel_variant):
         assert np.array_equal(sa[k], sb[k]), k
     assert N.lib().quad_step_range(b._h, n - 1, 2, C.c_void_p(acts.data_ptr()), C.byref(out), s) == N.QUAD_EINVAL
     a.close(); b.close()
+
+
+@pytest.mark.parametrize("env_name", ["hover", "trajectory"])
+def test_relpos_wrapper_is_base_obs_plus_prev_action(env_name):
+    """RelPosActWrapper (envs/wrappers.py:13-25): obs7 = [obs12[0:3], _prev_action]. Each step
+    starts both envs from the same state (re-synced), so the rel-pos part matches the unwrapped
+    env's to the parity bar (separately compiled kernels may differ by an ulp) and the flags
+    exactly; the previous action is the action just taken and zeros after a reset; observe and
+    get_state agree."""
+    n, T = 2048, 30
+    base = _env(n, env_name, None, seed=11, max_episode_steps=12)
+    rel = _env(n, env_name, "RelPosActWrapper", seed=11, max_episode_steps=12)
+    o12, o7 = base.reset(), rel.reset()
+    assert o7.shape == (n, 7) and torch.equal(o7[:, :3], o12[:, :3]) and torch.all(o7[:, 3:] == 0)
+    for t in range(T):
+        st = base.get_state()
+        st.pop("prev_action")
+        rel.set_state(**st)
+        a = base.random_actions(t)
+        o12, r12, te12, tr12, i12 = base.step(a)
+        o7, r7, te7, tr7, i7 = rel.step(a)
+        done = te12 | tr12
+        assert torch.equal(te7, te12) and torch.equal(tr7, tr12)
+        assert parity_ok(r7.cpu().numpy()[:, None], r12.cpu().numpy()[:, None]).all()
+        assert parity_ok(o7[:, :3].cpu().numpy(), o12[:, :3].cpu().numpy()).all()
+        assert torch.equal(o7[~done, 3:], a[~done]) and torch.all(o7[done, 3:] == 0)
+        tob7, tob12 = i7["terminal_observation"], i12["terminal_observation"]
+        assert parity_ok(tob7[done, :3].cpu().numpy(), tob12[done, :3].cpu().numpy()).all()
+        assert torch.equal(tob7[done, 3:], a[done])
+    assert torch.equal(rel.observe(torch.empty(n, 7, device="cuda")), o7)
+    g = rel.get_state()
+    assert np.array_equal(g["prev_action"], o7[:, 3:].cpu().numpy())

@@ -77,3 +77,28 @@ def test_short_training_makes_progress(fused):
         assert np.isfinite(ts["pg_loss"]) and np.isfinite(ts["vf_loss"])
     print("mean episode lengths", [round(x, 1) for x in lens])
     assert lens[-1] > 1.5 * lens[0]
+
+
+def test_train_cli_writes_reference_outputs(tmp_path):
+    """train.py outputs as the reference's consumers expect them: config.json with the
+    reference's keys (wrapper read by evaluate.py:316-321) and an SB3 archive."""
+    import json
+    import os
+    import zipfile
+    from uav_reinforcement_learning_control_amd import train
+    from uav_reinforcement_learning_control_amd.export import load_sb3_policy
+    for wrapper, dim in (("RateControlWrapper", 12), ("RelPosActWrapper", 7)):
+        md = tmp_path / wrapper
+        train.main(["--num-envs", "1024", "--total-timesteps", "30000", "--n-steps", "16",
+                    "--n-epochs", "1", "--n-minibatches", "2", "--wrapper", wrapper,
+                    "--log-dir", str(tmp_path / "logs"), "--model-dir", str(md)])
+        (run,) = os.listdir(md)
+        cfg = json.load(open(md / run / "config.json"))
+        for k in ("timestamp", "total_timesteps", "n_envs", "wrapper", "wrapper_source", "reward_function",
+                  "observation_function", "observation_bounds", "state_bounds", "target_pos_bounds", "ppo"):
+            assert k in cfg, k
+        assert cfg["wrapper"] == wrapper and cfg["ppo"]["n_steps"] == 16
+        z = md / run / "hover_policy_final.zip"
+        assert zipfile.is_zipfile(z)
+        pol = load_sb3_policy(str(z))
+        assert pol.mlp_extractor.policy_net[0].in_features == dim

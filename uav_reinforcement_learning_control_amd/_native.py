@@ -14,7 +14,7 @@ CSRC = os.path.join(_PKG, "csrc")
 
 QUAD_OK, QUAD_EINVAL, QUAD_EHIP, QUAD_ENOMEM, QUAD_EMODEL = 0, -1, -2, -3, -4
 ENV_HOVER, ENV_TRAJ, ENV_BRAX_HOVER, ENV_BRAX_TRAJ = 0, 1, 2, 3
-WRAP_NONE, WRAP_CTBR = 0, 1
+WRAP_NONE, WRAP_CTBR, WRAP_RELPOS = 0, 1, 2
 ABI_VERSION = 2
 
 
@@ -44,7 +44,7 @@ class QuadCfg(C.Structure):
 class QuadStateSoA(C.Structure):
     _fields_ = [("qpos", C.c_void_p), ("qvel", C.c_void_p), ("voltage", C.c_void_p),
                 ("target", C.c_void_p), ("rate_int", C.c_void_p), ("step_count", C.c_void_p),
-                ("episode", C.c_void_p)]
+                ("episode", C.c_void_p), ("prev_action", C.c_void_p)]
 
 
 class QuadStepOut(C.Structure):

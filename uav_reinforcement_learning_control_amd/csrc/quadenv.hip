@@ -31,8 +31,8 @@ using namespace quadenv;
 
 namespace {
 
-constexpr int NF = 28;
-constexpr int F_QPOS = 0, F_QVEL = 11, F_VOLT = 21, F_TGT = 22, F_RINT = 25;
+constexpr int NF = 32;
+constexpr int F_QPOS = 0, F_QVEL = 11, F_VOLT = 21, F_TGT = 22, F_RINT = 25, F_PREV = 28;
 constexpr int BLOCK = 256;
 
 thread_local std::string g_err;
@@ -196,6 +196,51 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, const float4* __restr
   store_obs_rows(lds, obs, out.obs, block_first, p.first + p.count);
 }
 
+
+// RelPosActWrapper (envs/wrappers.py:13-25) around HoverEnv / TrajectoryFollowEnv: the same step,
+// emitting obs7 = [obs[0:3], _prev_action] where _prev_action is the action just taken
+// (hover_env.py:166) and zeros after a reset (:212). The previous action is kept in the SoA
+// (F_PREV) so quad_observe / get_state stay exact.
+template <int KIND>
+__global__ __launch_bounds__(BLOCK) void k_step_relpos(KParams p, const float4* __restrict__ act,
+                                                       QuadStepOut out) {
+  const int i = p.first + blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= p.first + p.count) return;
+  EnvRegs<float> e;
+  load_env(p, i, e, false);
+  const float4 a4 = act[i];
+  const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+  StepRes r;
+  env_step<float, false>(p.k, e, a, r);
+  out.reward[i] = r.reward;
+  out.terminated[i] = r.term;
+  out.truncated[i] = r.trunc;
+  if (out.motor_commands)
+    reinterpret_cast<float4*>(out.motor_commands)[i] = make_float4(r.motor[0], r.motor[1], r.motor[2], r.motor[3]);
+  if (out.voltage_scale) out.voltage_scale[i] = r.vscale;
+  if (out.state12) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) out.state12[size_t(i) * 12 + j] = r.state12[j];
+  }
+  float o7[7] = {r.obs[0], r.obs[1], r.obs[2], a[0], a[1], a[2], a[3]};
+  float prev[4] = {a[0], a[1], a[2], a[3]};
+  if ((r.term || r.trunc) && p.auto_reset) {
+    if (out.terminal_obs) {
+#pragma unroll
+      for (int j = 0; j < 7; j++) out.terminal_obs[size_t(i) * 7 + j] = o7[j];
+    }
+    float obs12[12];
+    reset_env<KIND>(p, i, e, obs12);
+    o7[0] = obs12[0]; o7[1] = obs12[1]; o7[2] = obs12[2];
+#pragma unroll
+    for (int j = 0; j < 4; j++) { o7[3 + j] = 0.f; prev[j] = 0.f; }
+  }
+  store_env(p, i, e, false);
+#pragma unroll
+  for (int j = 0; j < 4; j++) p.soa[(F_PREV + j) * p.n + i] = prev[j];
+#pragma unroll
+  for (int j = 0; j < 7; j++) out.obs[size_t(i) * 7 + j] = o7[j];
+}
 
 // ---------------------------------------------------------------------------------------------
 // k_step_g<KIND, CTBR, G>: the step with one env per GROUP of G lanes (G = 1, 2, 4; 64/G envs
@@ -617,7 +662,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
   }
 }
 
-template <int KIND>
+template <int KIND, bool RELPOS>
 __global__ __launch_bounds__(BLOCK) void k_reset(KParams p, const uint8_t* __restrict__ mask,
                                                  float* __restrict__ obs_out) {
   const int i = blockIdx.x * BLOCK + threadIdx.x;
@@ -627,9 +672,16 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KParams p, const uint8_t* __res
   float obs[12];
   reset_env<KIND>(p, i, e, obs);
   store_env(p, i, e, true);
-  if (obs_out) {
 #pragma unroll
-    for (int j = 0; j < 12; j++) obs_out[size_t(i) * 12 + j] = obs[j];
+  for (int j = 0; j < 4; j++) p.soa[(F_PREV + j) * p.n + i] = 0.f;  // hover_env.py:212
+  if (obs_out) {
+    if (RELPOS) {
+#pragma unroll
+      for (int j = 0; j < 7; j++) obs_out[size_t(i) * 7 + j] = j < 3 ? obs[j] : 0.f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 12; j++) obs_out[size_t(i) * 12 + j] = obs[j];
+    }
   }
 }
 
@@ -696,6 +748,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe_brax(KParams p, float* __rest
   for (int j = 0; j < 21; j++) obs_out[size_t(i) * 21 + j] = s[(F_QPOS + j) * p.n + i];  // qpos, qvel
 }
 
+template <bool RELPOS>
 __global__ __launch_bounds__(BLOCK) void k_observe(KParams p, float* __restrict__ obs_out,
                                                    float* __restrict__ s12_out) {
   const int i = blockIdx.x * BLOCK + threadIdx.x;
@@ -704,8 +757,14 @@ __global__ __launch_bounds__(BLOCK) void k_observe(KParams p, float* __restrict_
   load_env(p, i, e, false);
   float obs[12], s12[12];
   observe(p.k, e, obs, s12);
+  if (RELPOS) {
 #pragma unroll
-  for (int j = 0; j < 12; j++) obs_out[size_t(i) * 12 + j] = obs[j];
+    for (int j = 0; j < 7; j++)
+      obs_out[size_t(i) * 7 + j] = j < 3 ? obs[j] : p.soa[(F_PREV + j - 3) * p.n + i];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 12; j++) obs_out[size_t(i) * 12 + j] = obs[j];
+  }
   if (s12_out) {
 #pragma unroll
     for (int j = 0; j < 12; j++) s12_out[size_t(i) * 12 + j] = s12[j];
@@ -788,7 +847,7 @@ int quad_default_cfg(int32_t env_kind, int32_t wrapper, QuadCfg* c) {
   if (!c) return fail(QUAD_EINVAL, "cfg is NULL");
   if (env_kind < QUAD_ENV_HOVER || env_kind > QUAD_ENV_BRAX_TRAJ)
     return fail(QUAD_EINVAL, "unknown env_kind");
-  if (wrapper != QUAD_WRAP_NONE && wrapper != QUAD_WRAP_CTBR) return fail(QUAD_EINVAL, "unknown wrapper");
+  if (wrapper < QUAD_WRAP_NONE || wrapper > QUAD_WRAP_RELPOS) return fail(QUAD_EINVAL, "unknown wrapper");
   if (env_kind >= QUAD_ENV_BRAX_HOVER && wrapper != QUAD_WRAP_NONE)
     return fail(QUAD_EINVAL, "the brax env kinds take no wrapper");
   std::memset(c, 0, sizeof *c);
@@ -860,7 +919,7 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
     return fail(QUAD_EINVAL, "n_envs too large");
   if (cfg->env_kind < QUAD_ENV_HOVER || cfg->env_kind > QUAD_ENV_BRAX_TRAJ)
     return fail(QUAD_EINVAL, "unknown env_kind");
-  if (cfg->wrapper != QUAD_WRAP_NONE && cfg->wrapper != QUAD_WRAP_CTBR)
+  if (cfg->wrapper < QUAD_WRAP_NONE || cfg->wrapper > QUAD_WRAP_RELPOS)
     return fail(QUAD_EINVAL, "unknown wrapper");
   if (cfg->env_kind >= QUAD_ENV_BRAX_HOVER && cfg->wrapper != QUAD_WRAP_NONE)
     return fail(QUAD_EINVAL, "the brax env kinds take no wrapper");
@@ -938,10 +997,14 @@ int quad_reset(QuadHandle* h, const uint8_t* mask, float* obs, void* stream) {
     hipLaunchKernelGGL(k_reset_brax<QUAD_ENV_BRAX_HOVER>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
   else if (h->cfg.env_kind == QUAD_ENV_BRAX_TRAJ)
     hipLaunchKernelGGL(k_reset_brax<QUAD_ENV_BRAX_TRAJ>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
+  else if (h->cfg.wrapper == QUAD_WRAP_RELPOS && h->cfg.env_kind == QUAD_ENV_TRAJ)
+    hipLaunchKernelGGL((k_reset<QUAD_ENV_TRAJ, true>), dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
+  else if (h->cfg.wrapper == QUAD_WRAP_RELPOS)
+    hipLaunchKernelGGL((k_reset<QUAD_ENV_HOVER, true>), dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
   else if (h->cfg.env_kind == QUAD_ENV_TRAJ)
-    hipLaunchKernelGGL(k_reset<QUAD_ENV_TRAJ>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
+    hipLaunchKernelGGL((k_reset<QUAD_ENV_TRAJ, false>), dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
   else
-    hipLaunchKernelGGL(k_reset<QUAD_ENV_HOVER>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
+    hipLaunchKernelGGL((k_reset<QUAD_ENV_HOVER, false>), dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
 }
@@ -971,7 +1034,13 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
   KParams kp = h->kp;
   kp.first = first;
   kp.count = count;
-  if (h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) {
+  if (h->cfg.wrapper == QUAD_WRAP_RELPOS) {
+    const dim3 grid(grid_of(count));
+    if (traj)
+      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_TRAJ>), grid, blk, 0, s, kp, a, *out);
+    else
+      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_HOVER>), grid, blk, 0, s, kp, a, *out);
+  } else if (h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) {
     const dim3 grid(grid_of(count));
     if (h->cfg.env_kind == QUAD_ENV_BRAX_TRAJ)
       hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_TRAJ>), grid, blk, 0, s, kp, a, *out);
@@ -1015,8 +1084,12 @@ int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream) {
     HIP_TRY(hipGetLastError());
     return QUAD_OK;
   }
-  hipLaunchKernelGGL(k_observe, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
-                     h->kp, obs, state12);
+  if (h->cfg.wrapper == QUAD_WRAP_RELPOS)
+    hipLaunchKernelGGL(k_observe<true>, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
+                       h->kp, obs, state12);
+  else
+    hipLaunchKernelGGL(k_observe<false>, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
+                       h->kp, obs, state12);
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
 }
@@ -1040,7 +1113,7 @@ static int copy_state(QuadHandle* h, const QuadStateSoA* u, int on_host, void* s
   const hipMemcpyKind kind = on_host ? (to_handle ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost)
                                      : hipMemcpyDeviceToDevice;
   struct Piece { void* user; void* mine; size_t bytes; };
-  const Piece pieces[7] = {
+  const Piece pieces[8] = {
       {u->qpos, h->soa + F_QPOS * n, 11 * n * sizeof(float)},
       {u->qvel, h->soa + F_QVEL * n, 10 * n * sizeof(float)},
       {u->voltage, h->soa + F_VOLT * n, n * sizeof(float)},
@@ -1048,6 +1121,7 @@ static int copy_state(QuadHandle* h, const QuadStateSoA* u, int on_host, void* s
       {u->rate_int, h->soa + F_RINT * n, 3 * n * sizeof(float)},
       {u->step_count, h->step, n * sizeof(int32_t)},
       {u->episode, h->ep, n * sizeof(uint32_t)},
+      {u->prev_action, h->soa + F_PREV * n, 4 * n * sizeof(float)},
   };
   for (const Piece& p : pieces) {
     if (!p.user) continue;

@@ -32,7 +32,7 @@ _ENV_KINDS = {"hover": N.ENV_HOVER, "HoverEnv": N.ENV_HOVER,
               "brax_jax_mjx": N.ENV_BRAX_TRAJ, "jax_mjx_quad": N.ENV_BRAX_TRAJ,
               "JaxMJXQuadBraxEnv": N.ENV_BRAX_TRAJ}
 _WRAPPERS = {None: N.WRAP_NONE, "none": N.WRAP_NONE, "RateControlWrapper": N.WRAP_CTBR,
-             "ctbr": N.WRAP_CTBR}
+             "ctbr": N.WRAP_CTBR, "RelPosActWrapper": N.WRAP_RELPOS, "relpos": N.WRAP_RELPOS}
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -82,9 +82,9 @@ class QuadVecEnv:
         self._h = h
         self.action_space = Box(-1.0, 1.0, (4,), np.float32)
         self.brax = cfg.env_kind >= N.ENV_BRAX_HOVER
-        self.obs_dim = 21 if self.brax else 12
+        self.obs_dim = 21 if self.brax else (7 if cfg.wrapper == N.WRAP_RELPOS else 12)
         self.observation_space = (Box(-np.inf, np.inf, (21,), np.float32) if self.brax
-                                  else Box(-1.0, 1.0, (12,), np.float32))
+                                  else Box(-1.0, 1.0, (self.obs_dim,), np.float32))
         n, dev = self.num_envs, self.device
         f32 = dict(dtype=torch.float32, device=dev)
         self.obs = torch.zeros(n, self.obs_dim, **f32)
@@ -191,7 +191,8 @@ class QuadVecEnv:
     # ------------------------------------------------------------------------------------
     _FIELDS = (("qpos", 11, np.float32), ("qvel", 10, np.float32), ("voltage", 1, np.float32),
                ("target", 3, np.float32), ("rate_int", 3, np.float32),
-               ("step_count", 1, np.int32), ("episode", 1, np.uint32))
+               ("step_count", 1, np.int32), ("episode", 1, np.uint32),
+               ("prev_action", 4, np.float32))
 
     def get_state(self) -> dict:
         """Env state as host numpy arrays, env-major ([N, fields])."""
@@ -203,7 +204,8 @@ class QuadVecEnv:
 
     def set_state(self, **fields) -> None:
         """Overwrite (some of) qpos [N,11], qvel [N,10], voltage [N], target [N,3],
-        rate_int [N,3], step_count [N], episode [N] (HoverEnv.set_state analogue)."""
+        rate_int [N,3], step_count [N], episode [N], prev_action [N,4] (HoverEnv.set_state
+        analogue)."""
         keep = []
         kw = {}
         for k, f, dt in self._FIELDS:

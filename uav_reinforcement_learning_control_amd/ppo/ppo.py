@@ -103,14 +103,15 @@ class PPO:
         self.device = env.device
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         torch.manual_seed(seed)  # identical policy init on every rank
-        self.policy = (policy or ActorCritic(12, 4, self.cfg.net_arch)).to(self.device)
+        self.obs_dim = int(getattr(env, "obs_dim", 12))
+        self.policy = (policy or ActorCritic(self.obs_dim, 4, self.cfg.net_arch)).to(self.device)
         self.params = [p for p in self.policy.parameters()]
         self.opt = torch.optim.Adam(self.params, lr=self.cfg.learning_rate, eps=self.cfg.adam_eps,
                                     fused=self.device.type == "cuda")  # one kernel per step
         torch.manual_seed(seed + 1000 * (dist.get_rank() if self.world > 1 else 0))
         T, n = self.cfg.n_steps, env.num_envs
         f32 = dict(dtype=torch.float32, device=self.device)
-        self.buf_obs = torch.zeros(T, n, 12, **f32)
+        self.buf_obs = torch.zeros(T, n, self.obs_dim, **f32)
         self.buf_act = torch.zeros(T, n, 4, **f32)
         self.buf_logp = torch.zeros(T, n, **f32)
         self.buf_val = torch.zeros(T, n, **f32)
@@ -118,7 +119,7 @@ class PPO:
         self.buf_start = torch.zeros(T, n, **f32)
         self.buf_adv = torch.zeros(T, n, **f32)
         self.buf_ret = torch.zeros(T, n, **f32)
-        self.last_obs = torch.zeros(n, 12, **f32)
+        self.last_obs = torch.zeros(n, self.obs_dim, **f32)
         self.last_start = torch.ones(n, **f32)
         self.ep_ret = torch.zeros(n, **f32)
         self.ep_len = torch.zeros(n, **f32)
@@ -136,7 +137,9 @@ class PPO:
         self._graph = None
         # fused path: cursor {t, pending} (buffer row = t % n_steps; t keys the action noise),
         # per-block episode-statistic slots, the epilogue descriptor
-        self._fp = FusedPolicy(self.policy) if self.cfg.fused_policy else None
+        # (the MFMA kernels are built for the 12-D HoverEnv obs and 128-128 nets)
+        fusable = self.obs_dim == 12 and tuple(self.cfg.net_arch) == (128, 128)
+        self._fp = FusedPolicy(self.policy) if self.cfg.fused_policy and fusable else None
         self._cursor = torch.zeros(4, dtype=torch.int32, device=self.device)
         self._slots = torch.zeros(N.POLICY_STAT_SLOTS, 3, dtype=torch.float64, device=self.device)
         if self._fp is not None:
@@ -245,7 +248,7 @@ class PPO:
     def train(self, n_epochs: Optional[int] = None, max_minibatches: Optional[int] = None) -> dict:
         cfg, pol = self.cfg, self.policy
         total = cfg.n_steps * self.env.num_envs
-        obs = self.buf_obs.view(total, 12)
+        obs = self.buf_obs.view(total, self.obs_dim)
         act = self.buf_act.view(total, 4)
         logp_old = self.buf_logp.view(total)
         adv_all = self.buf_adv.view(total)
