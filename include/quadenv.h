@@ -163,6 +163,40 @@ int quad_random_actions(QuadHandle* h, uint32_t step_index, float* actions, void
 int quad_get_state(QuadHandle* h, const QuadStateSoA* dst, int32_t on_host, void* stream);
 int quad_set_state(QuadHandle* h, const QuadStateSoA* src, int32_t on_host, void* stream);
 
+/* ---- Batched waypoint-following evaluation (row f4): evaluate.py:440-612 evaluate_trajectory
+ * for N envs at once (hover / trajectory kinds, any wrapper). Waypoint sets are float64 (the
+ * generators' numpy arrays) [n_sets][max_points][3]; env i follows set set_of[i] (0 if NULL). */
+typedef struct QuadWaypoints {
+  const double* points;    /* device [n_sets][max_points][3] */
+  const int32_t* counts;   /* device [n_sets], >= 1 */
+  const int32_t* set_of;   /* device [N] or NULL */
+  int32_t max_points;
+  float reach_radius;      /* --reach-radius (0.25) */
+} QuadWaypoints;
+/* Per-env tracker (device [N] arrays). status: 0 running, 1 lap completed, 2 terminated,
+ * 3 truncated (max steps). */
+typedef struct QuadWaypointState {
+  int32_t* wp_idx;
+  int32_t* reached;
+  int32_t* laps;
+  int32_t* steps;
+  int32_t* status;
+  double* total_reward;
+} QuadWaypointState;
+/* Start every env at its first waypoint (evaluate.py:487-505): qpos[0:7] = (wp0, 1, 0, 0, 0),
+ * qvel[0:6] = 0 (props keep their reset state), target = wp[1 % n], rate integrator 0, step 0;
+ * tracker zeroed with wp_idx = 1 % n; writes the observation (HoverEnv._get_obs, or the
+ * RelPosActWrapper observation) to obs. Call after quad_reset. */
+int quad_waypoints_begin(QuadHandle* h, const QuadWaypoints* w, const QuadWaypointState* s, float* obs,
+                         void* stream);
+/* After each quad_step (create the handle with auto_reset = 0): for envs still running, add the
+ * reward, count the step, switch to the next waypoint when |pos - wp| < reach_radius (pos =
+ * the step's state12[:, 0:3], info["state"]); completing the lap, terminated or truncated end
+ * the env's evaluation (evaluate.py:545-595). The next waypoint is written as the env target. */
+int quad_waypoints_update(QuadHandle* h, const QuadWaypoints* w, const QuadWaypointState* s,
+                          const float* state12, const float* reward, const uint8_t* terminated,
+                          const uint8_t* truncated, void* stream);
+
 /* PPO rollout support (row P of the scope table): generalized advantage estimation over a
  * time-major rollout, SB3 RolloutBuffer.compute_returns_and_advantage semantics.
  *  rewards, values, episode_starts: device [T,N] float32 (episode_starts 1.0 where the step

@@ -215,13 +215,36 @@ def rollout_fixture(kind: str, wrapper: bool, n_steps: int, seeds, max_episode_s
     return out
 
 
+def trajectories_fixture():
+    """utils/trajectories.py waypoint sets (evaluate.py's --trajectory options) for several
+    spacings / sizes / centers."""
+    from utils.trajectories import TRAJECTORY_GENERATORS as G
+    out = {}
+    for name, fn in G.items():
+        for spacing in (0.2, 0.5, 0.8):
+            out[f"{name}_s{spacing}"] = np.asarray(fn(spacing=spacing), np.float64)
+    out["eight_r1.5_c"] = np.asarray(G["eight"](spacing=0.3, radius=1.5, center=np.array([0.5, -0.2, 1.2])))
+    out["circle_r0.7_c"] = np.asarray(G["circle"](spacing=0.3, radius=0.7, center=np.array([0.1, 0.2, 0.8])))
+    out["square_l2_c"] = np.asarray(G["square"](spacing=0.3, side_length=2.0, center=np.array([-0.3, 0.0, 1.5])))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
+    ap.add_argument("--only", default=None, help="comma-separated fixture file names")
     args = ap.parse_args()
     _setup()
     os.makedirs(args.out, exist_ok=True)
+    if args.only:
+        lazy = {"golden_trajectories.npz": trajectories_fixture}
+        for name in args.only.split(","):
+            d = lazy[name]()
+            np.savez_compressed(os.path.join(args.out, name), **d)
+            print(name, {k: v.shape for k, v in d.items()})
+        return
     fx = {
+        "golden_trajectories.npz": trajectories_fixture(),
         "golden_euler.npz": euler_fixture(),
         "golden_termination.npz": termination_fixture(),
         "golden_hover_steps.npz": rollout_fixture("hover", False, 1500, range(100, 400)),

@@ -60,6 +60,15 @@ class QuadPolicyParams(C.Structure):
                                           "log_std")]
 
 
+class QuadWaypoints(C.Structure):
+    _fields_ = [("points", C.c_void_p), ("counts", C.c_void_p), ("set_of", C.c_void_p),
+                ("max_points", C.c_int32), ("reach_radius", C.c_float)]
+
+
+class QuadWaypointState(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("wp_idx", "reached", "laps", "steps", "status", "total_reward")]
+
+
 POLICY_STAT_SLOTS = 1024
 
 
@@ -83,7 +92,8 @@ class QuadPolicyAct(C.Structure):
 EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_create",
            "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
            "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
-           "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post")
+           "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post",
+           "quad_waypoints_begin", "quad_waypoints_update")
 
 
 class QuadError(RuntimeError):
@@ -117,9 +127,13 @@ def _declare(L):
     L.quad_policy_pack.argtypes = [C.POINTER(QuadPolicyParams), vp, vp]
     L.quad_policy_act.argtypes = [vp, C.POINTER(QuadPolicyAct), i32, vp]
     L.quad_rollout_post.argtypes = [vp, C.POINTER(QuadRolloutPost), vp, i32, vp]
+    L.quad_waypoints_begin.argtypes = [vp, C.POINTER(QuadWaypoints), C.POINTER(QuadWaypointState), vp, vp]
+    L.quad_waypoints_update.argtypes = [vp, C.POINTER(QuadWaypoints), C.POINTER(QuadWaypointState),
+                                        vp, vp, vp, vp, vp]
     for n in ("quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
-              "quad_policy_pack", "quad_policy_act", "quad_rollout_post"):
+              "quad_policy_pack", "quad_policy_act", "quad_rollout_post",
+              "quad_waypoints_begin", "quad_waypoints_update"):
         getattr(L, n).restype = C.c_int
 
 

@@ -771,6 +771,90 @@ __global__ __launch_bounds__(BLOCK) void k_observe(KParams p, float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// batched waypoint evaluation (evaluate.py:440-612)
+template <bool RELPOS>
+__global__ __launch_bounds__(BLOCK) void k_waypoints_begin(KParams p, QuadWaypoints w, QuadWaypointState t,
+                                                           float* __restrict__ obs_out) {
+  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= p.n) return;
+  const int set = w.set_of ? w.set_of[i] : 0;
+  const int cnt = w.counts[set];
+  const double* wp = w.points + size_t(set) * w.max_points * 3;
+  const int nxt = 1 % cnt;
+  const int n = p.n;
+  float* S = p.soa;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    S[(F_QPOS + j) * n + i] = float(wp[j]);
+    S[(F_QVEL + j) * n + i] = 0.f;
+    S[(F_QVEL + 3 + j) * n + i] = 0.f;
+    S[(F_TGT + j) * n + i] = float(wp[3 * nxt + j]);  // waypoints[i].astype(np.float32)
+    S[(F_RINT + j) * n + i] = 0.f;
+  }
+  S[(F_QPOS + 3) * n + i] = 1.f;
+  S[(F_QPOS + 4) * n + i] = 0.f;
+  S[(F_QPOS + 5) * n + i] = 0.f;
+  S[(F_QPOS + 6) * n + i] = 0.f;
+  p.step[i] = 0;
+  t.wp_idx[i] = nxt;
+  t.reached[i] = 0;
+  t.laps[i] = 0;
+  t.steps[i] = 0;
+  t.status[i] = 0;
+  t.total_reward[i] = 0.0;
+  EnvRegs<float> e;
+  load_env(p, i, e, false);
+  float obs[12], s12[12];
+  observe(p.k, e, obs, s12);
+  if (RELPOS) {
+#pragma unroll
+    for (int j = 0; j < 7; j++) obs_out[size_t(i) * 7 + j] = j < 3 ? obs[j] : S[(F_PREV + j - 3) * n + i];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 12; j++) obs_out[size_t(i) * 12 + j] = obs[j];
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_waypoints_update(KParams p, QuadWaypoints w, QuadWaypointState t,
+                                                            const float* __restrict__ s12,
+                                                            const float* __restrict__ rew,
+                                                            const uint8_t* __restrict__ term,
+                                                            const uint8_t* __restrict__ trunc) {
+  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= p.n || t.status[i] != 0) return;
+  const int set = w.set_of ? w.set_of[i] : 0;
+  const int cnt = w.counts[set];
+  const double* wp = w.points + size_t(set) * w.max_points * 3;
+  t.total_reward[i] += double(rew[i]);
+  t.steps[i] += 1;
+  int k = t.wp_idx[i];
+  // dist_to_wp = float(np.linalg.norm(drone_pos - current_target)): float32 pos minus the
+  // float64 waypoint, norm in float64
+  double d2 = 0.0;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const double d = double(s12[size_t(i) * 12 + j]) - wp[3 * k + j];
+    d2 += d * d;
+  }
+  int status = 0;
+  if (sqrt(d2) < double(w.reach_radius)) {
+    t.reached[i] += 1;
+    k = (k + 1) % cnt;
+    t.wp_idx[i] = k;
+    if (k == 0) {
+      t.laps[i] += 1;
+      status = 1;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 3; j++) p.soa[(F_TGT + j) * p.n + i] = float(wp[3 * k + j]);
+    }
+  }
+  if (status == 0 && term[i]) status = 2;
+  else if (status == 0 && trunc[i]) status = 3;
+  t.status[i] = status;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_random_actions(int32_t n, uint64_t seed, uint64_t gid_base,
                                                           uint32_t step, float4* __restrict__ act) {
   const int i = blockIdx.x * BLOCK + threadIdx.x;
@@ -1140,6 +1224,42 @@ int quad_get_state(QuadHandle* h, const QuadStateSoA* dst, int32_t on_host, void
 
 int quad_set_state(QuadHandle* h, const QuadStateSoA* src, int32_t on_host, void* stream) {
   return copy_state(h, src, on_host, stream, true);
+}
+
+static int check_waypoints(QuadHandle* h, const QuadWaypoints* w, const QuadWaypointState* s) {
+  if (!h || !w || !s) return fail(QUAD_EINVAL, "handle/waypoints/state is NULL");
+  if (!w->points || !w->counts || w->max_points < 1) return fail(QUAD_EINVAL, "waypoint table is empty");
+  if (!(w->reach_radius > 0.f)) return fail(QUAD_EINVAL, "reach_radius must be > 0");
+  if (!s->wp_idx || !s->reached || !s->laps || !s->steps || !s->status || !s->total_reward)
+    return fail(QUAD_EINVAL, "waypoint tracker arrays are required");
+  if (h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) return fail(QUAD_EINVAL, "waypoint evaluation needs a HoverEnv kind");
+  return QUAD_OK;
+}
+
+int quad_waypoints_begin(QuadHandle* h, const QuadWaypoints* w, const QuadWaypointState* s, float* obs,
+                         void* stream) {
+  if (int rc = check_waypoints(h, w, s)) return rc;
+  if (!obs) return fail(QUAD_EINVAL, "obs is NULL");
+  DeviceGuard g(h->device);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (h->cfg.wrapper == QUAD_WRAP_RELPOS)
+    hipLaunchKernelGGL(k_waypoints_begin<true>, dim3(grid_of(h->n)), dim3(BLOCK), 0, st, h->kp, *w, *s, obs);
+  else
+    hipLaunchKernelGGL(k_waypoints_begin<false>, dim3(grid_of(h->n)), dim3(BLOCK), 0, st, h->kp, *w, *s, obs);
+  HIP_TRY(hipGetLastError());
+  return QUAD_OK;
+}
+
+int quad_waypoints_update(QuadHandle* h, const QuadWaypoints* w, const QuadWaypointState* s,
+                          const float* state12, const float* reward, const uint8_t* terminated,
+                          const uint8_t* truncated, void* stream) {
+  if (int rc = check_waypoints(h, w, s)) return rc;
+  if (!state12 || !reward || !terminated || !truncated) return fail(QUAD_EINVAL, "step outputs are required");
+  DeviceGuard g(h->device);
+  hipLaunchKernelGGL(k_waypoints_update, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
+                     h->kp, *w, *s, state12, reward, terminated, truncated);
+  HIP_TRY(hipGetLastError());
+  return QUAD_OK;
 }
 
 int quad_gae(const float* rewards, const float* values, const float* episode_starts,
