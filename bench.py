@@ -297,12 +297,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob (tests only): run all ranks on one GPU over gloo, e.g. 2 ranks on a 1-GPU box
+    rehearsal = os.environ.get("QUAD_BENCH_REHEARSAL") == "1"
+    device_index = 0 if rehearsal else local_rank
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(device_index)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
 
-    res = _run_rank(args, rank, world, local_rank)
+    res = _run_rank(args, rank, world, device_index)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
