@@ -73,6 +73,11 @@ typedef struct QuadCfg {
   float vel_limit;              /* jax_mjx: any |v_i| > limit invalidates (20) */
   float traj_center[3], traj_amp[3], traj_freq[3];  /* jax_mjx sinusoid target */
   float traj_duration;          /* seconds spanned by the episode_length samples (5) */
+  /* TrajectoryFollowEnv's info-only spline (trajectory_follow_env.py:175-243): center ~
+   * U(spline_center_low, _high), n_wp ~ {3,4,5}, offsets ~ U(+-spline_amp), first waypoint = start
+   * position, natural cubic spline sampled at max_episode_steps points over spline_duration s. */
+  float spline_center_low[3], spline_center_high[3], spline_amp[3];
+  float spline_duration;        /* 30 */
 } QuadCfg;
 
 /* Env state in field-major SoA: each array is [fields][N] (qpos [11][N], qvel [10][N], ...).
@@ -103,7 +108,12 @@ typedef struct QuadStateSoA {
  *                        envs that finished this step are written
  *  motor_commands [N,4]  info["motor_commands"] (N)
  *  voltage_scale  [N]    info["voltage_scale"]
- *  state12        [N,12] info["state"]: absolute 12-D QuadState before auto-reset */
+ *  state12        [N,12] info["state"]: absolute 12-D QuadState before auto-reset
+ *  target_info    [N,9]  info["target"], ["target_vel"], ["target_acc"] before auto-reset: the
+ *                        TrajectoryFollowEnv spline sample at min(step - 1, L - 1)
+ *                        (trajectory_follow_env.py:163-168; regenerated from the episode's reset
+ *                        draw, so it follows quad_reset/auto-reset episodes, not injected states);
+ *                        the fixed target and zeros for the hover kinds */
 typedef struct QuadStepOut {
   float* obs;
   float* reward;
@@ -113,6 +123,7 @@ typedef struct QuadStepOut {
   float* motor_commands;
   float* voltage_scale;
   float* state12;
+  float* target_info;
 } QuadStepOut;
 
 typedef struct QuadHandle QuadHandle;

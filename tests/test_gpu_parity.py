@@ -354,3 +354,51 @@ def test_relpos_wrapper_is_base_obs_plus_prev_action(env_name):
     assert torch.equal(rel.observe(torch.empty(n, 7, device="cuda")), o7)
     g = rel.get_state()
     assert np.array_equal(g["prev_action"], o7[:, 3:].cpu().numpy())
+
+
+def _spline_ref(seed, gid, episode, start, step, L=2048, dur=30.0):
+    """TrajectoryFollowEnv._sample_sinusoid_trajectory restated with scipy (the device draw map:
+    Philox blocks 4..8 of the episode's reset counter)."""
+    from scipy.interpolate import CubicSpline
+    r = []
+    for blk in range(5):
+        r += O.philox([gid & 0xFFFFFFFF, gid >> 32, episode, 4 + blk], [seed & 0xFFFFFFFF, seed >> 32])
+    u = lambda x: np.float32((x >> 8) * 2.0 ** -24)
+    aff = lambda lo, uu, span: np.float32(np.float32(lo) + np.float32(uu * np.float32(span)))
+    nwp = 3 + (((r[3] >> 8) * 3) >> 24)
+    lo, hi, amp = [-1.0, -1.0, 0.4], [1.0, 1.0, 1.4], [0.6, 0.6, 0.4]
+    t = np.linspace(0.0, dur, L)[min(step - 1, L - 1)]
+    out = np.zeros(9)
+    for ax in range(3):
+        center = float(aff(lo[ax], u(r[ax]), np.float32(hi[ax]) - np.float32(lo[ax])))
+        y = np.array([center + float(aff(-amp[ax], u(r[4 + 5 * ax + i]), np.float32(2 * np.float32(amp[ax]))))
+                      for i in range(nwp)])
+        y[0] = float(start[ax])
+        cs = CubicSpline(np.linspace(0.0, dur, nwp), y, bc_type="natural")
+        out[ax], out[3 + ax], out[6 + ax] = cs(t), cs.derivative(1)(t), cs.derivative(2)(t)
+    return out
+
+
+def test_trajectory_info_spline_matches_scipy():
+    """info["target" / "target_vel" / "target_acc"] of TrajectoryFollowEnv
+    (trajectory_follow_env.py:163-168, :175-243) vs scipy's natural CubicSpline on the same draws."""
+    n, seed = 512, 21
+    env = _env(n, "trajectory", None, seed=seed, max_episode_steps=40)
+    env.reset()
+    starts = env.get_state()["target"].copy()      # traj_pos[0] = start position
+    eps = env.get_state()["episode"].copy()
+    for t in range(1, 46):
+        a = env.random_actions(t)
+        steps = env.get_state()["step_count"] + 1   # the step being taken, per env
+        _, _, te, tr, inf = env.step(a, info="full")
+        ti = torch.cat([inf["target"], inf["target_vel"], inf["target_acc"]], 1).cpu().numpy()
+        for i in range(0, n, 37):
+            ref = _spline_ref(seed, i, int(eps[i]) - 1, starts[i], int(steps[i]), L=40)
+            np.testing.assert_allclose(ti[i], ref, rtol=1e-6, atol=2e-6)
+        done = (te | tr).cpu().numpy()
+        if done.any():  # new episodes: new start position and draw counter
+            g = env.get_state()
+            starts[done] = g["target"][done]
+            eps[done] = g["episode"][done]
+        if t == 1:
+            np.testing.assert_allclose(ti[:, :3], starts, atol=1e-6)  # the spline starts at the start

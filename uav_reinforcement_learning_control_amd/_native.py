@@ -38,6 +38,8 @@ class QuadCfg(C.Structure):
         ("reward_action_coef", C.c_float), ("vel_limit", C.c_float),
         ("traj_center", C.c_float * 3), ("traj_amp", C.c_float * 3), ("traj_freq", C.c_float * 3),
         ("traj_duration", C.c_float),
+        ("spline_center_low", C.c_float * 3), ("spline_center_high", C.c_float * 3),
+        ("spline_amp", C.c_float * 3), ("spline_duration", C.c_float),
     ]
 
 
@@ -51,7 +53,7 @@ class QuadStepOut(C.Structure):
     _fields_ = [("obs", C.c_void_p), ("reward", C.c_void_p), ("terminated", C.c_void_p),
                 ("truncated", C.c_void_p), ("terminal_obs", C.c_void_p),
                 ("motor_commands", C.c_void_p), ("voltage_scale", C.c_void_p),
-                ("state12", C.c_void_p)]
+                ("state12", C.c_void_p), ("target_info", C.c_void_p)]
 
 
 class QuadPolicyParams(C.Structure):

@@ -170,6 +170,8 @@ struct KConsts {
   float bx_noise, bx_rpos, bx_ract, bx_vlim;
   float bx_tc[3], bx_ta[3], bx_tw[3];  // sinusoid center, amplitude, 2 pi f (float32 products)
   float bx_tdt, bx_tdur;               // linspace step dur / (L - 1), dur
+  // TrajectoryFollowEnv info spline
+  float sp_clo[3], sp_cspan[3], sp_amp[3], sp_dur;
 };
 
 template <typename T>
@@ -229,6 +231,12 @@ inline void make_kconsts(const QuadCfg& cfg, const PhysConstsD& d, KConsts<T>& k
     k.bx_tw[i] = float(2.0f * float(M_PI)) * cfg.traj_freq[i];  // (2.0 * jp.pi) * freq, float32
   }
   k.bx_tdur = cfg.traj_duration;
+  for (int i = 0; i < 3; i++) {
+    k.sp_clo[i] = cfg.spline_center_low[i];
+    k.sp_cspan[i] = cfg.spline_center_high[i] - cfg.spline_center_low[i];
+    k.sp_amp[i] = cfg.spline_amp[i];
+  }
+  k.sp_dur = cfg.spline_duration;
   k.bx_tdt = cfg.max_episode_steps > 1 ? cfg.traj_duration / float(cfg.max_episode_steps - 1) : 0.f;
 }
 
@@ -815,6 +823,68 @@ QD_HD void brax_reset_from(const KConsts<T>& k, EnvRegs<T>& e, const float u21[2
   for (int i = 0; i < 11; i++) obs21[i] = q[i];
 #pragma unroll
   for (int i = 0; i < 10; i++) obs21[11 + i] = u21[11 + i];
+}
+
+// ---------------------------------------------------------------------------------------------
+// TrajectoryFollowEnv info["target"/"target_vel"/"target_acc"] (trajectory_follow_env.py:163-168,
+// :175-216, :234-243): waypoints from Philox blocks 4..8 of the episode's reset counter (block 4:
+// center, n_wp; blocks 5..8: per-axis offsets, axis a uses values 5a..5a+n_wp-1), first waypoint =
+// start position, natural cubic spline in float64 (scipy CubicSpline bc_type="natural"), sampled
+// at t = linspace(0, duration, L)[min(step - 1, L - 1)].
+template <typename T>
+QD_HD void traj_spline_info(const KConsts<T>& k, uint64_t seed, uint64_t gid, uint32_t episode,
+                            const float start[3], int32_t step, float out9[9]) {
+  uint32_t r[20];
+#pragma unroll
+  for (uint32_t blk = 0; blk < 5; blk++) {
+    uint32_t c[4] = {uint32_t(gid), uint32_t(gid >> 32), episode, 4u + blk};
+    philox4x32_10(c, uint32_t(seed), uint32_t(seed >> 32));
+    r[4 * blk] = c[0]; r[4 * blk + 1] = c[1]; r[4 * blk + 2] = c[2]; r[4 * blk + 3] = c[3];
+  }
+  const int nwp = 3 + int((uint64_t(r[3] >> 8) * 3u) >> 24);  // integers(3, 6)
+  const int L = k.max_steps;
+  const int idx = (step - 1) < (L - 1) ? (step - 1 < 0 ? 0 : step - 1) : L - 1;
+  const double Td = double(k.sp_dur);
+  const double t = idx == L - 1 ? Td : double(idx) * (Td / double(L > 1 ? L - 1 : 1));
+  const double h = Td / double(nwp - 1);
+  int seg = int(t / h);
+  seg = seg < 0 ? 0 : (seg > nwp - 2 ? nwp - 2 : seg);
+  const double a = double(seg + 1) * h - t, b = t - double(seg) * h;  // t_{k+1} - t, t - t_k
+#pragma unroll
+  for (int ax = 0; ax < 3; ax++) {
+    const double center = double(affine32(k.sp_clo[ax], u01(r[ax]), k.sp_cspan[ax]));
+    double y[5];
+    for (int i = 0; i < 5; i++)
+      y[i] = center + double(affine32(-k.sp_amp[ax], u01(r[4 + 5 * ax + i]), 2.0f * k.sp_amp[ax]));
+    y[0] = double(start[ax]);
+    // natural spline second derivatives: M_0 = M_{n-1} = 0, M_{i-1} + 4 M_i + M_{i+1} = 6 d2y_i / h^2
+    double M[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    const double s6 = 6.0 / (h * h);
+    if (nwp == 3) {
+      M[1] = s6 * (y[2] - 2.0 * y[1] + y[0]) / 4.0;
+    } else {
+      // Thomas algorithm on the (nwp - 2) interior unknowns
+      double cp[3], dp[3];
+      const int m = nwp - 2;
+      for (int i = 0; i < m; i++) {
+        const double d = s6 * (y[i + 2] - 2.0 * y[i + 1] + y[i]);
+        const double den = i == 0 ? 4.0 : 4.0 - cp[i - 1];
+        cp[i] = 1.0 / den;
+        dp[i] = (d - (i == 0 ? 0.0 : dp[i - 1])) / den;
+      }
+      M[m] = dp[m - 1];
+      for (int i = m - 2; i >= 0; i--) M[i + 1] = dp[i] - cp[i] * M[i + 2];
+    }
+    const double Mk = M[seg], Mk1 = M[seg + 1], yk = y[seg], yk1 = y[seg + 1];
+    const double pos = Mk * a * a * a / (6.0 * h) + Mk1 * b * b * b / (6.0 * h) +
+                       (yk / h - Mk * h / 6.0) * a + (yk1 / h - Mk1 * h / 6.0) * b;
+    const double vel = -Mk * a * a / (2.0 * h) + Mk1 * b * b / (2.0 * h) - (yk / h - Mk * h / 6.0) +
+                       (yk1 / h - Mk1 * h / 6.0);
+    const double acc = Mk * a / h + Mk1 * b / h;
+    out9[ax] = float(pos);
+    out9[3 + ax] = float(vel);
+    out9[6 + ax] = float(acc);
+  }
 }
 
 }  // namespace quadenv

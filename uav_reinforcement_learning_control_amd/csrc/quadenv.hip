@@ -157,6 +157,17 @@ __device__ __forceinline__ void store_obs_rows(float4* lds, const float obs[12],
   }
 }
 
+// info["target", "target_vel", "target_acc"] of the step just taken (before any auto-reset)
+template <int KIND>
+__device__ __forceinline__ void write_target_info(const KParams& p, int i, const EnvRegs<float>& e,
+                                                  float* __restrict__ out) {
+  float o[9] = {e.target[0], e.target[1], e.target[2], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (KIND == QUAD_ENV_TRAJ)  // the target register holds the start position (= traj_pos[0])
+    traj_spline_info(p.k, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, e.target, e.step, o);
+#pragma unroll
+  for (int j = 0; j < 9; j++) out[size_t(i) * 9 + j] = o[j];
+}
+
 template <int KIND, bool CTBR>
 __global__ __launch_bounds__(BLOCK) void k_step(KParams p, const float4* __restrict__ act,
                                                 QuadStepOut out) {
@@ -182,6 +193,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, const float4* __restr
 #pragma unroll
       for (int j = 0; j < 12; j++) out.state12[size_t(i) * 12 + j] = r.state12[j];
     }
+    if (out.target_info) write_target_info<KIND>(p, i, e, out.target_info);
 #pragma unroll
     for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
     if ((r.term || r.trunc) && p.auto_reset) {
@@ -222,6 +234,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_relpos(KParams p, const float4* 
 #pragma unroll
     for (int j = 0; j < 12; j++) out.state12[size_t(i) * 12 + j] = r.state12[j];
   }
+  if (out.target_info) write_target_info<KIND>(p, i, e, out.target_info);
   float o7[7] = {r.obs[0], r.obs[1], r.obs[2], a[0], a[1], a[2], a[3]};
   float prev[4] = {a[0], a[1], a[2], a[3]};
   if ((r.term || r.trunc) && p.auto_reset) {
@@ -707,6 +720,10 @@ __global__ __launch_bounds__(BLOCK) void k_step_brax(KParams p, const float4* __
   if (out.motor_commands)
     reinterpret_cast<float4*>(out.motor_commands)[i] = make_float4(motor[0], motor[1], motor[2], motor[3]);
   if (out.voltage_scale) out.voltage_scale[i] = 1.0f;
+  if (out.target_info) {
+#pragma unroll
+    for (int j = 0; j < 9; j++) out.target_info[size_t(i) * 9 + j] = j < 3 ? e.target[j] : 0.f;
+  }
   if ((term || trunc) && p.auto_reset) {
     if (out.terminal_obs) {
 #pragma unroll
@@ -977,6 +994,13 @@ int quad_default_cfg(int32_t env_kind, int32_t wrapper, QuadCfg* c) {
   c->gravity[2] = -9.81;
   c->density = 1.225;
   c->viscosity = 1.8e-5;
+  {  // TrajectoryFollowEnv spline (trajectory_follow_env.py:25, :55-58, :199-203)
+    const float lo[3] = {-1.f, -1.f, 0.4f}, hi[3] = {1.f, 1.f, 1.4f}, amp[3] = {0.6f, 0.6f, 0.4f};
+    for (int i = 0; i < 3; i++) {
+      c->spline_center_low[i] = lo[i]; c->spline_center_high[i] = hi[i]; c->spline_amp[i] = amp[i];
+    }
+    c->spline_duration = 30.f;
+  }
   if (env_kind >= QUAD_ENV_BRAX_HOVER) {  // train_brax_ppo.py
     const bool traj = env_kind == QUAD_ENV_BRAX_TRAJ;
     c->max_episode_steps = 500;                        // --episode-length (:436)
@@ -1114,7 +1138,7 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
   const float4* a = reinterpret_cast<const float4*>(actions);
   const bool traj = h->cfg.env_kind == QUAD_ENV_TRAJ, ctbr = h->cfg.wrapper == QUAD_WRAP_CTBR;
   const dim3 blk(BLOCK);
-  const int G = h->lanes;
+  const int G = out->target_info ? 0 : h->lanes;  // info mode: the one-thread form carries it
   KParams kp = h->kp;
   kp.first = first;
   kp.count = count;

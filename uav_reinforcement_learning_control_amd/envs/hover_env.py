@@ -91,9 +91,12 @@ class HoverEnv:
         st = self._sync_state()
         info = {"state": self._state.vec(),
                 "motor_commands": inf["motor_commands"].cpu().numpy()[0].astype(np.float64),
-                "target": self.target_state.position.copy(),
+                "target": inf["target"].cpu().numpy()[0].copy(),
                 "voltage": float(st["voltage"][0]),
                 "voltage_scale": float(inf["voltage_scale"].cpu().numpy()[0])}
+        if self._KIND == "trajectory":  # trajectory_follow_env.py:163-168 (spline sample)
+            info["target_vel"] = inf["target_vel"].cpu().numpy()[0].copy()
+            info["target_acc"] = inf["target_acc"].cpu().numpy()[0].copy()
         return obs, float(r.cpu().numpy()[0]), bool(te.cpu()[0]), bool(tr.cpu()[0]), info
 
     def set_state(self, qpos, qvel):

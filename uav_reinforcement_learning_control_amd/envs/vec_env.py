@@ -95,6 +95,7 @@ class QuadVecEnv:
         self.motor_commands = torch.zeros(n, 4, **f32)
         self.voltage_scale = torch.zeros(n, **f32)
         self.state12 = torch.zeros(n, 12, **f32)
+        self.target_info = torch.zeros(n, 9, **f32)
 
     # ------------------------------------------------------------------------------------
     def _stream(self):
@@ -142,7 +143,8 @@ class QuadVecEnv:
         actions: float32 [N,4] on the env's device (not clipped by the env, like HoverEnv).
         The returned tensors are the env's own buffers (overwritten by the next step) unless
         obs/reward are given. info="basic": terminal_observation + TimeLimit.truncated;
-        info="full": also motor_commands, voltage_scale, state (HoverEnv's info dict);
+        info="full": also motor_commands, voltage_scale, state, target (+ target_vel / target_acc:
+        TrajectoryFollowEnv's spline sample) -- HoverEnv's / TrajectoryFollowEnv's info dict;
         info="raw": terminal_observation only (no extra device op; for graph-captured loops).
         """
         self._check(actions, (self.num_envs, 4), torch.float32)
@@ -157,7 +159,8 @@ class QuadVecEnv:
             terminal_obs=self.terminal_obs.data_ptr(),
             motor_commands=self.motor_commands.data_ptr() if full else None,
             voltage_scale=self.voltage_scale.data_ptr() if full else None,
-            state12=self.state12.data_ptr() if full and not self.brax else None)
+            state12=self.state12.data_ptr() if full and not self.brax else None,
+            target_info=self.target_info.data_ptr() if full else None)
         N.check(N.lib().quad_step(self._h, C.c_void_p(actions.data_ptr()), C.byref(o),
                                   self._stream()), "quad_step")
         inf = {"terminal_observation": self.terminal_obs}
@@ -165,7 +168,8 @@ class QuadVecEnv:
             inf["TimeLimit.truncated"] = self.truncated & ~self.terminated
         if full:
             inf.update(motor_commands=self.motor_commands, voltage_scale=self.voltage_scale,
-                       state=self.state12)
+                       state=self.state12, target=self.target_info[:, 0:3],
+                       target_vel=self.target_info[:, 3:6], target_acc=self.target_info[:, 6:9])
         return obs, reward, self.terminated, self.truncated, inf
 
     def observe(self, out: Optional[torch.Tensor] = None, state: bool = False):
