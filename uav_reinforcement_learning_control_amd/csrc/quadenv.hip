@@ -63,7 +63,7 @@ int hip_fail(hipError_t e, const char* what) {
   } while (0)
 
 struct KParams {
-  KConsts<float> k;
+  const KConsts<float>* __restrict__ kc;  // per-handle constant block in device memory
   float* soa;
   int32_t* step;
   uint32_t* ep;
@@ -133,9 +133,9 @@ __device__ __forceinline__ void reset_env(const KParams& p, int i, EnvRegs<float
                                           float obs[12]) {
   const uint32_t ep = p.ep[i];
   float init12[12], tgt[3], s12[12];
-  reset_draw(p.k.init_lo, p.k.init_span, p.k.tgt_lo, p.k.tgt_span, p.seed, p.gid_base + uint64_t(i),
+  reset_draw(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, p.seed, p.gid_base + uint64_t(i),
              ep, init12, tgt);
-  env_reset_from<float, KIND>(p.k, e, init12, tgt, obs, s12);
+  env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
   p.ep[i] = ep + 1;
 }
 
@@ -163,7 +163,7 @@ __device__ __forceinline__ void write_target_info(const KParams& p, int i, const
                                                   float* __restrict__ out) {
   float o[9] = {e.target[0], e.target[1], e.target[2], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (KIND == QUAD_ENV_TRAJ)  // the target register holds the start position (= traj_pos[0])
-    traj_spline_info(p.k, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, e.target, e.step, o);
+    traj_spline_info(*p.kc, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, e.target, e.step, o);
 #pragma unroll
   for (int j = 0; j < 9; j++) out[size_t(i) * 9 + j] = o[j];
 }
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, const float4* __restr
     const float4 a4 = act[i];
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
     StepRes r;
-    env_step<float, CTBR>(p.k, e, a, r);
+    env_step<float, CTBR>(*p.kc, e, a, r);
     out.reward[i] = r.reward;
     out.terminated[i] = r.term;
     out.truncated[i] = r.trunc;
@@ -223,7 +223,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_relpos(KParams p, const float4* 
   const float4 a4 = act[i];
   const float a[4] = {a4.x, a4.y, a4.z, a4.w};
   StepRes r;
-  env_step<float, false>(p.k, e, a, r);
+  env_step<float, false>(*p.kc, e, a, r);
   out.reward[i] = r.reward;
   out.terminated[i] = r.term;
   out.truncated[i] = r.trunc;
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
   if (G > 1 && i_raw >= end) return;
   const bool live = i_raw < end;
   const unsigned i = live ? i_raw : end - 1;
-  const KConsts<float>& k = p.k;
+  const KConsts<float>& k = *p.kc;
   const PhysConsts<float>& c = k.ph;
   const size_t n = size_t(p.n);
   const float* __restrict__ S = p.soa;
@@ -713,7 +713,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_brax(KParams p, const float4* __
   const float a[4] = {a4.x, a4.y, a4.z, a4.w};
   float obs[21], reward, motor[4];
   bool term, trunc;
-  brax_step<float, KIND>(p.k, e, a, obs, reward, term, trunc, motor);
+  brax_step<float, KIND>(*p.kc, e, a, obs, reward, term, trunc, motor);
   out.reward[i] = reward;
   out.terminated[i] = term;
   out.truncated[i] = trunc;
@@ -730,8 +730,8 @@ __global__ __launch_bounds__(BLOCK) void k_step_brax(KParams p, const float4* __
       for (int j = 0; j < 21; j++) out.terminal_obs[size_t(i) * 21 + j] = obs[j];
     }
     float u21[21];
-    brax_reset_draw(p.k.bx_noise, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, u21);
-    brax_reset_from<float, KIND>(p.k, e, u21, obs, true);
+    brax_reset_draw(p.kc->bx_noise, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, u21);
+    brax_reset_from<float, KIND>(*p.kc, e, u21, obs, true);
   }
   store_env(p, i, e, true);
 #pragma unroll
@@ -746,9 +746,9 @@ __global__ __launch_bounds__(BLOCK) void k_reset_brax(KParams p, const uint8_t* 
   if (mask && !mask[i]) return;
   const uint32_t ep = p.ep[i];
   float u21[21], obs[21];
-  brax_reset_draw(p.k.bx_noise, p.seed, p.gid_base + uint64_t(i), ep, u21);
+  brax_reset_draw(p.kc->bx_noise, p.seed, p.gid_base + uint64_t(i), ep, u21);
   EnvRegs<float> e;
-  brax_reset_from<float, KIND>(p.k, e, u21, obs, false);
+  brax_reset_from<float, KIND>(*p.kc, e, u21, obs, false);
   p.ep[i] = ep + 1u;
   store_env(p, i, e, true);
   if (obs_out) {
@@ -773,7 +773,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(KParams p, float* __restrict_
   EnvRegs<float> e;
   load_env(p, i, e, false);
   float obs[12], s12[12];
-  observe(p.k, e, obs, s12);
+  observe(*p.kc, e, obs, s12);
   if (RELPOS) {
 #pragma unroll
     for (int j = 0; j < 7; j++)
@@ -823,7 +823,7 @@ __global__ __launch_bounds__(BLOCK) void k_waypoints_begin(KParams p, QuadWaypoi
   EnvRegs<float> e;
   load_env(p, i, e, false);
   float obs[12], s12[12];
-  observe(p.k, e, obs, s12);
+  observe(*p.kc, e, obs, s12);
   if (RELPOS) {
 #pragma unroll
     for (int j = 0; j < 7; j++) obs_out[size_t(i) * 7 + j] = j < 3 ? obs[j] : S[(F_PREV + j - 3) * n + i];
@@ -919,6 +919,8 @@ struct QuadHandle {
   float* soa = nullptr;
   int32_t* step = nullptr;
   uint32_t* ep = nullptr;
+  KConsts<float> kh;                 // host copy of the constant block
+  KConsts<float>* kdev = nullptr;    // device copy the kernels read (scalar loads, K$-resident)
 };
 
 namespace {
@@ -1043,7 +1045,7 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
     delete h;
     return fail(QUAD_EMODEL, why);
   }
-  make_kconsts<float>(*cfg, h->pd, h->kp.k);
+  make_kconsts<float>(*cfg, h->pd, h->kh);
   h->device = device;
   h->n = n_envs;
   DeviceGuard g(device);
@@ -1053,11 +1055,14 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   if (e == hipSuccess) e = hipMemset(h->soa, 0, sizeof(float) * size_t(NF) * n_envs);
   if (e == hipSuccess) e = hipMemset(h->step, 0, sizeof(int32_t) * size_t(n_envs));
   if (e == hipSuccess) e = hipMemset(h->ep, 0, sizeof(uint32_t) * size_t(n_envs));
+  if (e == hipSuccess) e = hipMalloc(&h->kdev, sizeof(KConsts<float>));
+  if (e == hipSuccess) e = hipMemcpy(h->kdev, &h->kh, sizeof(KConsts<float>), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     quad_destroy(h);
     return hip_fail(e, "quad_create allocation");
   }
+  h->kp.kc = h->kdev;
   h->kp.soa = h->soa;
   h->kp.step = h->step;
   h->kp.ep = h->ep;
@@ -1084,6 +1089,7 @@ void quad_destroy(QuadHandle* h) {
   if (h->soa) (void)hipFree(h->soa);
   if (h->step) (void)hipFree(h->step);
   if (h->ep) (void)hipFree(h->ep);
+  if (h->kdev) (void)hipFree(h->kdev);
   delete h;
 }
 
