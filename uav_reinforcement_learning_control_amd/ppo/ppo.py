@@ -204,9 +204,12 @@ class PPO:
         torch.cuda.current_stream(self.device).wait_stream(s)
         self._t.zero_()
         self._cursor.zero_()
+        # several steps per graph (the step index lives on the device), fewer replay gaps
+        self._graph_steps = next(k for k in (16, 8, 4, 2, 1) if self.cfg.n_steps % k == 0)
         self._graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._graph):
-            step()
+            for _ in range(self._graph_steps):
+                step()
         torch.cuda.synchronize(self.device)
 
     @torch.no_grad()
@@ -225,10 +228,11 @@ class PPO:
         self._done_stats.zero_()
         step = self._step_fn()
         self._slots.zero_()
-        for _ in range(cfg.n_steps):
-            if use_graph and self._graph is not None:
+        if use_graph and self._graph is not None:
+            for _ in range(cfg.n_steps // self._graph_steps):
                 self._graph.replay()
-            else:
+        else:
+            for _ in range(cfg.n_steps):
                 step()
         if self._fp is not None:
             self._fp.post(self._epi, self._cursor)   # finish the last step
