@@ -402,3 +402,77 @@ def test_trajectory_info_spline_matches_scipy():
             eps[done] = g["episode"][done]
         if t == 1:
             np.testing.assert_allclose(ti[:, :3], starts, atol=1e-6)  # the spline starts at the start
+
+
+@pytest.mark.parametrize("n", [1, 255, 257, 4097])
+def test_ragged_sizes_match_oracle(n, kernel_variant):
+    """Batch sizes that are not a multiple of the 256-thread block (and a single env) step every
+    env exactly once, in every kernel form; rows past N are never touched."""
+    rng = np.random.default_rng(n)
+    st = _random_states(n, rng)
+    acts = rng.uniform(-1, 1, (n, 4)).astype(np.float32)
+    env = _env(n, "hover", "RateControlWrapper", auto_reset=False)
+    env.set_state(**st)
+    a = torch.from_numpy(acts).cuda()
+    obs = torch.full((n + 7, 12), 7.0, device="cuda")  # sentinel rows after the batch
+    env.step(a, obs=obs[:n])
+    torch.cuda.synchronize()
+    assert torch.all(obs[n:] == 7.0)
+    ref = _oracle_step(O.ENV_HOVER, O.WRAP_CTBR, st, acts)
+    got = obs[:n].cpu().numpy()
+    assert all(parity_ok(got[i], ref[i]["obs"]) for i in range(n))
+    env.close()
+
+
+def test_four_million_envs_properties():
+    """A 4,194,304-env batch (index arithmetic far past 2^16 blocks): every row finite, rewards in
+    (0, 1], flags consistent with the state bounds, a strided oracle sample exact."""
+    n = 1 << 22
+    env = _env(n, seed=5)
+    env.reset()
+    acts = env.random_actions(0)
+    pre = env.get_state()
+    obs, rew, te, tr, inf = env.step(acts, info="full")
+    torch.cuda.synchronize()
+    assert torch.isfinite(obs).all() and ((rew > 0) & (rew <= 1)).all()
+    s12 = inf["state"]
+    lo = torch.tensor(env.cfg.term_low[:], device="cuda:0")
+    hi = torch.tensor(env.cfg.term_high[:], device="cuda:0")
+    assert torch.equal(~(((s12 >= lo) & (s12 <= hi)).all(dim=1)), te)
+    a = acts.cpu().numpy(); o_obs = obs.cpu().numpy(); tob = inf["terminal_observation"].cpu().numpy()
+    ten = te.cpu().numpy()
+    cfg = O.default_cfg(O.ENV_HOVER, O.WRAP_NONE)
+    for i in list(range(0, n, n // 256)) + [n - 1]:
+        e = O.Env(cfg=cfg)
+        e.set_full_state(pre["qpos"][i], pre["qvel"][i], pre["voltage"][i], pre["target"][i],
+                         pre["step_count"][i])
+        o = O.out_to_dict(e.step(a[i]))
+        assert o["terminated"] == bool(ten[i])
+        assert parity_ok(tob[i] if ten[i] else o_obs[i], o["obs"])
+    env.close()
+
+
+def test_invalid_arguments_fail_cleanly():
+    import ctypes as C
+    from uav_reinforcement_learning_control_amd import _native as N
+    L = N.lib()
+    cfg = N.default_cfg()
+    h = C.c_void_p()
+    for n in (0, -5, 1 << 30):
+        assert L.quad_create(C.byref(cfg), 0, 0, 0, n, C.byref(h)) == N.QUAD_EINVAL and not h.value
+    bad = N.default_cfg()
+    bad.max_episode_steps = 0
+    assert L.quad_create(C.byref(bad), 0, 0, 0, 16, C.byref(h)) == N.QUAD_EINVAL
+    assert L.quad_create(C.byref(cfg), 99, 0, 0, 16, C.byref(h)) == N.QUAD_EINVAL
+    env = _env(64)
+    a = torch.zeros(64, 4, device="cuda")
+    out = N.QuadStepOut(obs=None, reward=env.reward.data_ptr(), terminated=env.terminated.data_ptr(),
+                        truncated=env.truncated.data_ptr())
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert L.quad_step(env._h, C.c_void_p(a.data_ptr()), C.byref(out), s) == N.QUAD_EINVAL
+    out.obs = env.obs.data_ptr()
+    assert L.quad_step_range(env._h, 60, 8, C.c_void_p(a.data_ptr()), C.byref(out), s) == N.QUAD_EINVAL
+    assert L.quad_step(env._h, C.c_void_p(a.data_ptr() + 4), C.byref(out), s) == N.QUAD_EINVAL
+    assert b"aligned" in L.quad_last_error()
+    assert L.quad_step(env._h, C.c_void_p(a.data_ptr()), C.byref(out), s) == N.QUAD_OK
+    env.close()

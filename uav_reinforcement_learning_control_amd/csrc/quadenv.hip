@@ -571,6 +571,12 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
         out.state12[size_t(i) * 12 + 3 * m + j] = G == 1 ? s12[3 * it + j] : pick4(m, s12[j], s12[3 + j], s12[6 + j], s12[9 + j]);
     }
   }
+  if (out.target_info && live && l == 0) {  // info target (+ spline velocity / acceleration)
+    float o[9] = {tgt[0], tgt[1], tgt[2], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (KIND == QUAD_ENV_TRAJ) traj_spline_info(k, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, tgt, step, o);
+#pragma unroll
+    for (int j = 0; j < 9; j++) out.target_info[size_t(i) * 9 + j] = o[j];
+  }
   // ---- SB3 auto-reset (group-uniform branch)
   const bool reset = (term || trunc) && p.auto_reset;
   if (reset) {
@@ -1144,7 +1150,7 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
   const float4* a = reinterpret_cast<const float4*>(actions);
   const bool traj = h->cfg.env_kind == QUAD_ENV_TRAJ, ctbr = h->cfg.wrapper == QUAD_WRAP_CTBR;
   const dim3 blk(BLOCK);
-  const int G = out->target_info ? 0 : h->lanes;  // info mode: the one-thread form carries it
+  const int G = h->lanes;
   KParams kp = h->kp;
   kp.first = first;
   kp.count = count;
