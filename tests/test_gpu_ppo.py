@@ -102,3 +102,35 @@ def test_train_cli_writes_reference_outputs(tmp_path):
         assert zipfile.is_zipfile(z)
         pol = load_sb3_policy(str(z))
         assert pol.mlp_extractor.policy_net[0].in_features == dim
+
+
+def test_brax_profile_ppo_trains_and_exports(tmp_path):
+    """Brax-profile learner on the jax_mjx_quad kind: losses finite, timesteps counted like brax
+    (batch_size * unroll_length * num_minibatches per training step), episode reward improves,
+    and the CLI writes ppo_params.msgpack + training_summary.json that load back."""
+    import json
+    import os
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    from uav_reinforcement_learning_control_amd.export import load_brax_params
+    from uav_reinforcement_learning_control_amd.ppo.brax_ppo import BraxPPO, BraxPPOConfig
+    from uav_reinforcement_learning_control_amd import train_brax
+    cfg = BraxPPOConfig(num_envs=2048, batch_size=512, num_minibatches=8, episode_length=200)
+    env = QuadVecEnv(2048, env="brax_jax_mjx", device="cuda:0", seed=0, max_episode_steps=200)
+    m = BraxPPO(env, cfg, seed=0)
+    curve = []
+    for it in range(40):
+        st = m.training_step()
+        assert st.env_steps == 512 * 10 * 8
+        assert all(np.isfinite(v) for v in st.losses.values())
+        curve.append(st.mean_episode_reward)
+    print("brax-profile episode reward", [round(c, 2) for c in curve if np.isfinite(c)][::4])
+    fin = [c for c in curve if np.isfinite(c)]
+    assert np.mean(fin[-5:]) > np.mean(fin[:5])
+    train_brax.main(["--env", "jax_mjx_quad", "--num-envs", "1024", "--batch-size", "256",
+                     "--num-minibatches", "8", "--num-timesteps", "60000", "--checkpoint-interval", "20000",
+                     "--output-dir", str(tmp_path)])
+    (run,) = os.listdir(tmp_path)
+    summ = json.load(open(tmp_path / run / "training_summary.json"))
+    norm, pol, val = load_brax_params(summ["params_path"])
+    assert norm["count"] > 0 and pol["params"]["hidden_2"]["kernel"].shape == (128, 8)
+    assert len(os.listdir(tmp_path / run / "checkpoints")) >= 2

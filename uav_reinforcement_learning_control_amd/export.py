@@ -24,9 +24,12 @@ archive structure, the opcode-level pickle contents and the weights round trip.
 ``load_sb3_policy`` reads a reference-trained archive's ``policy.pth`` (``torch.load(...,
 weights_only=True)``; nothing in the archive is unpickled) into an ``ActorCritic``.
 
-Brax ``ppo_params.msgpack`` (train_brax_ppo.py:624-625) is not produced: brax's ``save_params``
-pickles flax/brax objects for a tanh-Normal policy with observation normalization, a different
-policy family from this SB3-style Gaussian learner (DESIGN.md "Out of scope").
+``save_brax_params`` writes what brax's ``model.save_params`` writes for ``ppo.train``'s result
+(train_brax_ppo.py:580-581, :624-625): a pickle of ``(RunningStatisticsState, policy, value)``
+with flax-style ``{"params": {"hidden_i": {"kernel": [in, out], "bias"}}}`` trees (numpy leaves),
+for the brax-profile learner (ppo/brax_ppo.py); ``brax.io.model.load_params`` and
+evaluate_brax_ppo.py's ``make_inference_fn(...)(params)`` consume it. ``load_brax_params`` reads such
+files back through an allow-list unpickler (numpy arrays and that one class only).
 """
 from __future__ import annotations
 
@@ -109,6 +112,7 @@ class _FakeModules:
 
 _POLICY_CLS = _stand_in("stable_baselines3.common.policies", "ActorCriticPolicy")
 _BOX_CLS = _stand_in("gymnasium.spaces.box", "Box")
+_RSS_CLS = _stand_in("brax.training.acme.running_statistics", "RunningStatisticsState")
 
 
 def _box(low: np.ndarray, high: np.ndarray):
@@ -256,3 +260,53 @@ def load_sb3_policy(path: str, device="cpu") -> ActorCritic:
     pol = ActorCritic(obs_dim, act_dim, tuple(arch))
     pol.load_state_dict(sd, strict=True)
     return pol.to(device)
+
+
+# ---- brax params ("ppo_params.msgpack") -------------------------------------------------------
+def _tree_refs(tree):
+    if isinstance(tree, dict):
+        return {k: _tree_refs(v) for k, v in tree.items()}
+    return _ArrayRef(np.asarray(tree, np.float32))
+
+
+def save_brax_params(path: str, params) -> str:
+    """brax ``model.save_params(path, (normalizer, policy, value))`` for BraxPPO.params()."""
+    norm, pol, val = params
+    if getattr(_RSS_CLS, "_stand_in", False):
+        rss = _RSS_CLS.__new__(_RSS_CLS)
+        rss.__dict__.update({k: _ArrayRef(np.asarray(norm[k], np.float32))
+                             for k in ("mean", "std", "count", "summed_variance")})
+    else:  # brax installed: the real flax dataclass
+        rss = _RSS_CLS(mean=np.asarray(norm["mean"], np.float32), std=np.asarray(norm["std"], np.float32),
+                       count=np.asarray(norm["count"], np.float32),
+                       summed_variance=np.asarray(norm["summed_variance"], np.float32))
+    with _FakeModules([_RSS_CLS]):
+        raw = pickle.dumps((rss, _tree_refs(pol), _tree_refs(val)), protocol=_PICKLE_PROTOCOL)
+    with open(path, "wb") as f:
+        f.write(raw)
+    return path
+
+
+class _BraxParamsUnpickler(pickle.Unpickler):
+    class _RSS:
+        def __setstate__(self, state):
+            self.__dict__.update(state)
+
+    def find_class(self, module, name):
+        if (module, name) == ("brax.training.acme.running_statistics", "RunningStatisticsState"):
+            return self._RSS
+        if (module, name) in (("numpy", "array"), ("numpy", "dtype"), ("copyreg", "__newobj__")):
+            import copyreg
+            return copyreg.__newobj__ if module == "copyreg" else getattr(np, name)
+        if (module, name) in (("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+                              ("numpy", "ndarray")):
+            return np.core.multiarray._reconstruct if name == "_reconstruct" else np.ndarray
+        raise pickle.UnpicklingError(f"refusing {module}.{name} in a params file")
+
+
+def load_brax_params(path: str):
+    """(normalizer dict, policy tree, value tree) from a params file with numpy leaves."""
+    with open(path, "rb") as f:
+        rss, pol, val = _BraxParamsUnpickler(f).load()
+    norm = {k: np.asarray(getattr(rss, k)) for k in ("mean", "std", "count", "summed_variance")}
+    return norm, pol, val
