@@ -137,7 +137,8 @@ int quad_default_cfg(int32_t env_kind, int32_t wrapper, QuadCfg* cfg);
 /* Allocate N envs on `device`. Global env ids are env_id_base .. env_id_base+N-1; the reset RNG
  * is Philox4x32-10 keyed by `seed` with counter (global env id, episode, draw block), so a
  * shard's trajectories do not depend on how many GPUs the envs are spread over.
- * State starts zeroed; call quad_reset before stepping. */
+ * State starts zeroed; call quad_reset before stepping. 1 <= N <= 33,554,431 (the state SoA is
+ * addressed as one 4 GiB buffer resource); QUAD_EINVAL otherwise. */
 int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_id_base,
                 int32_t n_envs, QuadHandle** out);
 void quad_destroy(QuadHandle* h);

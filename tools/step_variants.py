@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Profiling tool (not product): the step kernel's cost by part at N envs -- the in-tree library
+against the ablation builds of tools/step_variants.sh (physics twice / none, no observation, no
+auto-reset, no SLP vectorizer), graph-replayed with random actions, HIP-event timed (bench.py's method). The marginal
+cost of a part = time(variant) - time(base). Prints one line per variant."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    lanes = sys.argv[2] if len(sys.argv) > 2 else "0"
+    variants = ["base", "PHYS2", "NOPHYS", "NOOBS", "NORESET", "SLP"]
+    if len(sys.argv) > 3 and sys.argv[3] == "child":
+        return child(n, lanes, variants[int(sys.argv[4])])
+    for k, v in enumerate(variants):  # one process per variant: the library is loaded once per process
+        r = subprocess.run([sys.executable, __file__, str(n), lanes, "child", str(k)], capture_output=True,
+                           text=True, timeout=300)
+        print(r.stdout.strip() or r.stderr.strip()[-400:], flush=True)
+
+
+def child(n, lanes, v):
+    os.environ["QUADENV_LANES"] = lanes
+    from uav_reinforcement_learning_control_amd import _native as N
+    if v != "base":
+        N.LIB_PATH = os.path.join(ROOT, "tools", "_build", f"abl_{v}.so")
+    from tools.lanes_sweep import run
+    us = [run(int(lanes), n, steps=400) for _ in range(3)]
+    print(f"{v:8s} n={n} lanes={lanes}: {min(us):.2f} us/step (runs {', '.join(f'{u:.2f}' for u in us)})")
+
+
+if __name__ == "__main__":
+    main()

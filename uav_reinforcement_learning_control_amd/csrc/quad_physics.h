@@ -614,9 +614,25 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
   const double load = ((F[0] + F[1] + F[2] + F[3]) * 0.25) * k.r_mx;
   const double dV = (k.vb + k.vl * load) * k.dt;
   e.volt = T(clipn(double(e.volt) - dV, k.vmin, k.vnom));
+  // QD_ABL_*: cost-ablation builds of tools/step_variants.py only (never defined in the product)
+#if defined(QD_ABL_PHYS2)
   physics_step(k.ph, e, F);
+  physics_step(k.ph, e, F);
+#elif !defined(QD_ABL_NOPHYS)
+  physics_step(k.ph, e, F);
+#endif
   e.step += 1;
+#if defined(QD_ABL_NOOBS)
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    r.state12[i] = float(e.pos[i]); r.state12[3 + i] = float(e.q[1 + i]);
+    r.state12[6 + i] = float(e.v[i]); r.state12[9 + i] = float(e.w[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 12; i++) r.obs[i] = r.state12[i];
+#else
   observe(k, e, r.obs, r.state12);
+#endif
   r.reward = reward_of<T>(r.state12, e.target);
   r.term = terminated_of(k, r.state12);
   r.trunc = e.step >= k.max_steps;
@@ -646,21 +662,26 @@ QD_HD float affine32(float lo, float u, float span) {
 }
 
 // Draws for HoverEnv.reset: 12 init-state values then 3 target values (QuadState.random_reset +
-// the target draw, hover_env.py:219-228), Philox-keyed by (seed; global env id, episode, block).
+// the target draw, hover_env.py:219-228), Philox-keyed by (seed; global env id, episode, block):
+// word j of the draw is word j % 4 of block j / 4.
+QD_HD void reset_block(uint64_t seed, uint64_t gid, uint32_t episode, uint32_t blk, uint32_t c[4]) {
+  c[0] = uint32_t(gid); c[1] = uint32_t(gid >> 32); c[2] = episode; c[3] = blk;
+  philox4x32_10(c, uint32_t(seed), uint32_t(seed >> 32));
+}
+QD_HD void reset_affine(const float init_lo[12], const float init_span[12], const float tgt_lo[3],
+                        const float tgt_span[3], const uint32_t r[16], float init12[12], float tgt[3]) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) init12[i] = affine32(init_lo[i], u01(r[i]), init_span[i]);
+#pragma unroll
+  for (int i = 0; i < 3; i++) tgt[i] = affine32(tgt_lo[i], u01(r[12 + i]), tgt_span[i]);
+}
 QD_HD void reset_draw(const float init_lo[12], const float init_span[12], const float tgt_lo[3],
                       const float tgt_span[3], uint64_t seed, uint64_t gid, uint32_t episode,
                       float init12[12], float tgt[3]) {
   uint32_t r[16];
 #pragma unroll
-  for (uint32_t blk = 0; blk < 4; blk++) {
-    uint32_t c[4] = {uint32_t(gid), uint32_t(gid >> 32), episode, blk};
-    philox4x32_10(c, uint32_t(seed), uint32_t(seed >> 32));
-    r[4 * blk] = c[0]; r[4 * blk + 1] = c[1]; r[4 * blk + 2] = c[2]; r[4 * blk + 3] = c[3];
-  }
-#pragma unroll
-  for (int i = 0; i < 12; i++) init12[i] = affine32(init_lo[i], u01(r[i]), init_span[i]);
-#pragma unroll
-  for (int i = 0; i < 3; i++) tgt[i] = affine32(tgt_lo[i], u01(r[12 + i]), tgt_span[i]);
+  for (uint32_t blk = 0; blk < 4; blk++) reset_block(seed, gid, episode, blk, r + 4 * blk);
+  reset_affine(init_lo, init_span, tgt_lo, tgt_span, r, init12, tgt);
 }
 
 // HoverEnv.reset / TrajectoryFollowEnv.reset given the draws; writes the reset obs.

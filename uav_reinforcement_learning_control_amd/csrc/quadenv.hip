@@ -31,8 +31,14 @@ using namespace quadenv;
 
 namespace {
 
-constexpr int NF = 32;
+// Env state layout in HBM: tiles of 64 envs (one wave), each tile NFT fields x 64 lanes of 4 B
+// (8,704 B). Field f of env i lives at (i / 64) * TILE_BYTES + f * 256 + (i % 64) * 4: a wave's
+// accesses to one field are 256 contiguous bytes, and every field is an immediate offset from one
+// per-lane byte offset (see Tiles).
 constexpr int F_QPOS = 0, F_QVEL = 11, F_VOLT = 21, F_TGT = 22, F_RINT = 25, F_PREV = 28;
+constexpr int F_STEP = 32, F_EP = 33;  // int32 step count, uint32 episode counter
+constexpr int NFT = 34;
+constexpr uint32_t TILE_BYTES = NFT * 64 * 4;
 constexpr int BLOCK = 256;
 
 thread_local std::string g_err;
@@ -64,10 +70,9 @@ int hip_fail(hipError_t e, const char* what) {
 
 struct KParams {
   const KConsts<float>* __restrict__ kc;  // per-handle constant block in device memory
-  float* soa;
-  int32_t* step;
-  uint32_t* ep;
-  int32_t n;      // envs in the handle (SoA stride)
+  float* tiles;         // env state tiles (layout above)
+  uint32_t tile_bytes;  // bytes of all tiles (< 4 GiB: one buffer resource)
+  int32_t n;      // envs in the handle
   int32_t first;  // step launches cover envs [first, first + count)
   int32_t count;
   int32_t auto_reset;
@@ -75,69 +80,167 @@ struct KParams {
   uint64_t gid_base;
 };
 
+// ---- addressing. All env state goes through ONE buffer resource and one per-lane byte offset
+// (env_off); the field offset f * 256 splits into the instruction's 12-bit immediate and a constant
+// SGPR (0 / 4096 / 8192), so a step's 60 state loads and stores need no address arithmetic and
+// no address registers. (Plain [field][n] indexing gave each field a 64-bit VGPR address, computed
+// for the load burst and held until the matching store: ~54 VGPRs and 2 waves per SIMD.) Other
+// per-env arrays use the global saddr form: uniform base + 32-bit byte offset.
+__device__ __forceinline__ uint32_t env_off(uint32_t i) { return (i >> 6) * TILE_BYTES + (i & 63u) * 4u; }
+struct Tiles {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ explicit Tiles(const KParams& p)
+      : r(__builtin_amdgcn_make_buffer_rsrc(p.tiles, 0, int(p.tile_bytes), 0x00020000)) {}
+  // f must fold to a constant (unrolled loops): a lane-varying f would make the SGPR part divergent
+  __device__ __forceinline__ uint32_t ldu(int f, uint32_t vo) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, 0);
+  }
+  __device__ __forceinline__ void stu(int f, uint32_t vo, uint32_t x) const {
+    __builtin_amdgcn_raw_buffer_store_b32(x, r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, 0);
+  }
+  __device__ __forceinline__ float ld(int f, uint32_t vo) const { return __builtin_bit_cast(float, ldu(f, vo)); }
+  __device__ __forceinline__ void st(int f, uint32_t vo, float x) const { stu(f, vo, __builtin_bit_cast(uint32_t, x)); }
+  // lane-varying field (k_step_g with G > 1): the whole offset in the VGPR
+  __device__ __forceinline__ float ldv(int f, uint32_t vo) const {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f) * 256u, 0, 0));
+  }
+  __device__ __forceinline__ void stv(int f, uint32_t vo, float x) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), r, vo + uint32_t(f) * 256u, 0, 0);
+  }
+};
+template <typename T>
+__device__ __forceinline__ T ldo(const T* b, uint32_t off) {
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(b) + off);
+}
+template <typename T>
+__device__ __forceinline__ void sto(T* b, uint32_t off, T v) {
+  *reinterpret_cast<T*>(reinterpret_cast<char*>(b) + off) = v;
+}
+
 __device__ __forceinline__ void load_env(const KParams& p, int i, EnvRegs<float>& e, bool ctbr) {
-  const int n = p.n;
-  const float* s = p.soa;
+  const Tiles S(p);
+  const uint32_t o = env_off(uint32_t(i));
 #pragma unroll
-  for (int j = 0; j < 3; j++) e.pos[j] = s[(F_QPOS + j) * n + i];
+  for (int j = 0; j < 3; j++) e.pos[j] = S.ld(F_QPOS + j, o);
 #pragma unroll
-  for (int j = 0; j < 4; j++) e.q[j] = s[(F_QPOS + 3 + j) * n + i];
+  for (int j = 0; j < 4; j++) e.q[j] = S.ld(F_QPOS + 3 + j, o);
 #pragma unroll
-  for (int j = 0; j < 4; j++) e.th[j] = s[(F_QPOS + 7 + j) * n + i];
+  for (int j = 0; j < 4; j++) e.th[j] = S.ld(F_QPOS + 7 + j, o);
 #pragma unroll
-  for (int j = 0; j < 3; j++) e.v[j] = s[(F_QVEL + j) * n + i];
+  for (int j = 0; j < 3; j++) e.v[j] = S.ld(F_QVEL + j, o);
 #pragma unroll
-  for (int j = 0; j < 3; j++) e.w[j] = s[(F_QVEL + 3 + j) * n + i];
+  for (int j = 0; j < 3; j++) e.w[j] = S.ld(F_QVEL + 3 + j, o);
 #pragma unroll
-  for (int j = 0; j < 4; j++) e.s[j] = s[(F_QVEL + 6 + j) * n + i];
-  e.volt = s[F_VOLT * n + i];
+  for (int j = 0; j < 4; j++) e.s[j] = S.ld(F_QVEL + 6 + j, o);
+  e.volt = S.ld(F_VOLT, o);
 #pragma unroll
-  for (int j = 0; j < 3; j++) e.target[j] = s[(F_TGT + j) * n + i];
+  for (int j = 0; j < 3; j++) e.target[j] = S.ld(F_TGT + j, o);
   if (ctbr) {
 #pragma unroll
-    for (int j = 0; j < 3; j++) e.rint[j] = s[(F_RINT + j) * n + i];
+    for (int j = 0; j < 3; j++) e.rint[j] = S.ld(F_RINT + j, o);
   } else {
     e.rint[0] = e.rint[1] = e.rint[2] = 0.f;
   }
-  e.step = p.step[i];
+  e.step = int32_t(S.ldu(F_STEP, o));
 }
 
 __device__ __forceinline__ void store_env(const KParams& p, int i, const EnvRegs<float>& e,
                                           bool ctbr) {
-  const int n = p.n;
-  float* s = p.soa;
+  const Tiles S(p);
+  const uint32_t o = env_off(uint32_t(i));
 #pragma unroll
-  for (int j = 0; j < 3; j++) s[(F_QPOS + j) * n + i] = e.pos[j];
+  for (int j = 0; j < 3; j++) S.st(F_QPOS + j, o, e.pos[j]);
 #pragma unroll
-  for (int j = 0; j < 4; j++) s[(F_QPOS + 3 + j) * n + i] = e.q[j];
+  for (int j = 0; j < 4; j++) S.st(F_QPOS + 3 + j, o, e.q[j]);
 #pragma unroll
-  for (int j = 0; j < 4; j++) s[(F_QPOS + 7 + j) * n + i] = e.th[j];
+  for (int j = 0; j < 4; j++) S.st(F_QPOS + 7 + j, o, e.th[j]);
 #pragma unroll
-  for (int j = 0; j < 3; j++) s[(F_QVEL + j) * n + i] = e.v[j];
+  for (int j = 0; j < 3; j++) S.st(F_QVEL + j, o, e.v[j]);
 #pragma unroll
-  for (int j = 0; j < 3; j++) s[(F_QVEL + 3 + j) * n + i] = e.w[j];
+  for (int j = 0; j < 3; j++) S.st(F_QVEL + 3 + j, o, e.w[j]);
 #pragma unroll
-  for (int j = 0; j < 4; j++) s[(F_QVEL + 6 + j) * n + i] = e.s[j];
-  s[F_VOLT * n + i] = e.volt;
+  for (int j = 0; j < 4; j++) S.st(F_QVEL + 6 + j, o, e.s[j]);
+  S.st(F_VOLT, o, e.volt);
 #pragma unroll
-  for (int j = 0; j < 3; j++) s[(F_TGT + j) * n + i] = e.target[j];
+  for (int j = 0; j < 3; j++) S.st(F_TGT + j, o, e.target[j]);
   if (ctbr) {
 #pragma unroll
-    for (int j = 0; j < 3; j++) s[(F_RINT + j) * n + i] = e.rint[j];
+    for (int j = 0; j < 3; j++) S.st(F_RINT + j, o, e.rint[j]);
   }
-  p.step[i] = e.step;
+  S.stu(F_STEP, o, uint32_t(e.step));
 }
 
+// The reset draw of episode `ep` (the env's counter, loaded by the caller with the state); the
+// caller stores ep + 1 after its other stores. Step kernels issue every global store after this:
+// a store ahead of the constant-block reads would make them VMEM loads (the compiler can no
+// longer rule out a clobber), each with a vmcnt wait that on gfx9 also drains the stores.
 template <int KIND>
-__device__ __forceinline__ void reset_env(const KParams& p, int i, EnvRegs<float>& e,
-                                          float obs[12]) {
-  const uint32_t ep = p.ep[i];
+__device__ __forceinline__ void reset_env(const KParams& p, int i, EnvRegs<float>& e, float obs[12],
+                                          uint32_t ep) {
   float init12[12], tgt[3], s12[12];
   reset_draw(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, p.seed, p.gid_base + uint64_t(i),
              ep, init12, tgt);
   env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
-  p.ep[i] = ep + 1;
 }
+
+// The reset draws of a wave's resetting envs, compacted: each resetting lane publishes (env,
+// episode) under its rank among them, every lane of the wave then computes one (env, block) Philox
+// item, and the resetting lanes read back their 16 words. With <= 16 resets per wave (the common
+// case) that is one Philox pass for the wave instead of four serial ones per resetting lane: a
+// Philox block is 20 quarter-rate v_mad_u64_u32, and the draw was half the reset branch.
+// Identical words to reset_draw (same counters). Called by every active lane of the wave.
+struct ResetLds {
+  uint32_t env[4][64], ep[4][64];
+  uint4 words[4][256];  // [wave][rank * 4 + block]
+};
+__device__ __forceinline__ void reset_words_wave(const KParams& p, ResetLds& L, uint32_t i, uint32_t ep,
+                                                 bool rs, uint32_t r16[16]) {
+  const uint64_t m = __ballot(rs);
+  if (m == 0) return;
+  const int w = threadIdx.x >> 6, lane = __lane_id();
+  const int nres = __popcll(m);
+  const int rank = __popcll(m & __lanemask_lt());
+  if (rs) { L.env[w][rank] = i; L.ep[w][rank] = ep; }
+  __builtin_amdgcn_wave_barrier();
+  const int passes = (nres * 4 + 63) >> 6;
+  for (int t = 0; t < passes; t++) {
+    const int item = t * 64 + lane, rr = item >> 2;
+    if (rr < nres) {
+      uint32_t c[4];
+      reset_block(p.seed, p.gid_base + uint64_t(L.env[w][rr]), L.ep[w][rr], uint32_t(item & 3), c);
+      L.words[w][item] = make_uint4(c[0], c[1], c[2], c[3]);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (rs) {
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint4 v = L.words[w][rank * 4 + b];
+      r16[4 * b] = v.x; r16[4 * b + 1] = v.y; r16[4 * b + 2] = v.z; r16[4 * b + 3] = v.w;
+    }
+  }
+}
+
+// One 12-float row per lane: three 16-byte stores when the row base is 16-byte aligned (a uniform
+// test), else twelve dword stores. Row-per-lane stores are issue-bound: 12 scattered dword
+// stores per lane cost the wave far more issue time than 3 dwordx4.
+__device__ __forceinline__ void store_row12(float* __restrict__ base, uint32_t i, const float v[12]) {
+  if ((reinterpret_cast<uintptr_t>(base) & 15u) == 0) {
+    float4* b4 = reinterpret_cast<float4*>(base);
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+      sto(b4, 48u * i + 16u * j, make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 12; j++) sto(base, 48u * i + 4u * j, v[j]);
+  }
+}
+
+// Mark a loaded value as consumed here, before the step's first store. gfx9's vmcnt retires
+// loads and stores in issue order: a value first read AFTER stores were issued (the episode
+// counter, read only by the reset branch) makes its s_waitcnt drain those stores too -- a store
+// round trip on every wave that resets.
+__device__ __forceinline__ void settle(uint32_t x) { asm volatile("" ::"v"(x)); }
 
 // Stage the block's [256,12] obs rows through LDS; write them as contiguous float4.
 __device__ __forceinline__ void store_obs_rows(float4* lds, const float obs[12], float* out,
@@ -157,51 +260,72 @@ __device__ __forceinline__ void store_obs_rows(float4* lds, const float obs[12],
   }
 }
 
-// info["target", "target_vel", "target_acc"] of the step just taken (before any auto-reset)
+// info["target", "target_vel", "target_acc"] of the step just taken (before any auto-reset);
+// `ep` is the episode counter as loaded (the running episode is ep - 1)
 template <int KIND>
-__device__ __forceinline__ void write_target_info(const KParams& p, int i, const EnvRegs<float>& e,
-                                                  float* __restrict__ out) {
-  float o[9] = {e.target[0], e.target[1], e.target[2], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (KIND == QUAD_ENV_TRAJ)  // the target register holds the start position (= traj_pos[0])
-    traj_spline_info(*p.kc, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, e.target, e.step, o);
+__device__ __forceinline__ void target_info_of(const KParams& p, int i, const EnvRegs<float>& e,
+                                               uint32_t ep, float o[9]) {
+  o[0] = e.target[0]; o[1] = e.target[1]; o[2] = e.target[2];
 #pragma unroll
-  for (int j = 0; j < 9; j++) out[size_t(i) * 9 + j] = o[j];
+  for (int j = 3; j < 9; j++) o[j] = 0.f;
+  if (KIND == QUAD_ENV_TRAJ)  // the target register holds the start position (= traj_pos[0])
+    traj_spline_info(*p.kc, p.seed, p.gid_base + uint64_t(i), ep - 1u, e.target, e.step, o);
+}
+
+__device__ __forceinline__ void store_target_info(float* __restrict__ out, int i, const float o[9]) {
+#pragma unroll
+  for (int j = 0; j < 9; j++) sto(out, uint32_t(i) * 36u + 4u * j, o[j]);
 }
 
 template <int KIND, bool CTBR>
-__global__ __launch_bounds__(BLOCK) void k_step(KParams p, const float4* __restrict__ act,
-                                                QuadStepOut out) {
+__global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict__ kc, KParams p,
+                                                const float4* __restrict__ act, QuadStepOut out) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores below (see KParams)
   __shared__ float4 lds[BLOCK * 3];
+  __shared__ ResetLds rl;
   const int block_first = p.first + blockIdx.x * BLOCK;
   const int i = block_first + threadIdx.x;
   float obs[12];
   if (i < p.first + p.count) {
     EnvRegs<float> e;
     load_env(p, i, e, CTBR);
+    const Tiles S(p);
+    const uint32_t vo = env_off(uint32_t(i));
+    const uint32_t ep = S.ldu(F_EP, vo);
     const float4 a4 = act[i];
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
     StepRes r;
     env_step<float, CTBR>(*p.kc, e, a, r);
-    out.reward[i] = r.reward;
-    out.terminated[i] = r.term;
-    out.truncated[i] = r.trunc;
+    settle(ep);
+    const uint32_t o = uint32_t(i) * 4u;
+    sto(out.reward, o, r.reward);
+    sto(out.terminated, uint32_t(i), uint8_t(r.term));
+    sto(out.truncated, uint32_t(i), uint8_t(r.trunc));
     if (out.motor_commands)
-      reinterpret_cast<float4*>(out.motor_commands)[i] =
-          make_float4(r.motor[0], r.motor[1], r.motor[2], r.motor[3]);
-    if (out.voltage_scale) out.voltage_scale[i] = r.vscale;
-    if (out.state12) {
-#pragma unroll
-      for (int j = 0; j < 12; j++) out.state12[size_t(i) * 12 + j] = r.state12[j];
+      sto(reinterpret_cast<float4*>(out.motor_commands), 4u * o,
+          make_float4(r.motor[0], r.motor[1], r.motor[2], r.motor[3]));
+    if (out.voltage_scale) sto(out.voltage_scale, o, r.vscale);
+    if (out.state12) store_row12(out.state12, uint32_t(i), r.state12);
+    if (out.target_info) {
+      float info[9];
+      target_info_of<KIND>(p, i, e, ep, info);
+      store_target_info(out.target_info, i, info);
     }
-    if (out.target_info) write_target_info<KIND>(p, i, e, out.target_info);
 #pragma unroll
     for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
-    if ((r.term || r.trunc) && p.auto_reset) {
-      if (out.terminal_obs) {
-#pragma unroll
-        for (int j = 0; j < 12; j++) out.terminal_obs[size_t(i) * 12 + j] = r.obs[j];
-      }
-      reset_env<KIND>(p, i, e, obs);
+#if defined(QD_ABL_NORESET)
+    const bool rs = false;
+#else
+    const bool rs = (r.term || r.trunc) && p.auto_reset;
+#endif
+    uint32_t r16[16];
+    reset_words_wave(p, rl, uint32_t(i), ep, rs, r16);
+    if (rs) {
+      if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
+      float init12[12], tgt[3], s12[12];
+      reset_affine(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, r16, init12, tgt);
+      env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
+      S.stu(F_EP, vo, ep + 1u);
     }
     store_env(p, i, e, CTBR);
   }
@@ -214,16 +338,28 @@ __global__ __launch_bounds__(BLOCK) void k_step(KParams p, const float4* __restr
 // (hover_env.py:166) and zeros after a reset (:212). The previous action is kept in the SoA
 // (F_PREV) so quad_observe / get_state stay exact.
 template <int KIND>
-__global__ __launch_bounds__(BLOCK) void k_step_relpos(KParams p, const float4* __restrict__ act,
-                                                       QuadStepOut out) {
+__global__ __launch_bounds__(BLOCK) void k_step_relpos(const KConsts<float>* __restrict__ kc, KParams p,
+                                                       const float4* __restrict__ act, QuadStepOut out) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
   const int i = p.first + blockIdx.x * BLOCK + threadIdx.x;
   if (i >= p.first + p.count) return;
   EnvRegs<float> e;
   load_env(p, i, e, false);
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
+  const uint32_t ep = S.ldu(F_EP, vo);
   const float4 a4 = act[i];
   const float a[4] = {a4.x, a4.y, a4.z, a4.w};
   StepRes r;
   env_step<float, false>(*p.kc, e, a, r);
+  float info[9];
+  if (out.target_info) target_info_of<KIND>(p, i, e, ep, info);
+  float o7[7] = {r.obs[0], r.obs[1], r.obs[2], a[0], a[1], a[2], a[3]};
+  float prev[4] = {a[0], a[1], a[2], a[3]};
+  const bool rs = (r.term || r.trunc) && p.auto_reset;
+  float obs12[12];
+  if (rs) reset_env<KIND>(p, i, e, obs12, ep);
+  // ---- every global store after the reset (see reset_env)
   out.reward[i] = r.reward;
   out.terminated[i] = r.term;
   out.truncated[i] = r.trunc;
@@ -234,23 +370,20 @@ __global__ __launch_bounds__(BLOCK) void k_step_relpos(KParams p, const float4* 
 #pragma unroll
     for (int j = 0; j < 12; j++) out.state12[size_t(i) * 12 + j] = r.state12[j];
   }
-  if (out.target_info) write_target_info<KIND>(p, i, e, out.target_info);
-  float o7[7] = {r.obs[0], r.obs[1], r.obs[2], a[0], a[1], a[2], a[3]};
-  float prev[4] = {a[0], a[1], a[2], a[3]};
-  if ((r.term || r.trunc) && p.auto_reset) {
+  if (out.target_info) store_target_info(out.target_info, i, info);
+  if (rs) {
     if (out.terminal_obs) {
 #pragma unroll
       for (int j = 0; j < 7; j++) out.terminal_obs[size_t(i) * 7 + j] = o7[j];
     }
-    float obs12[12];
-    reset_env<KIND>(p, i, e, obs12);
+    S.stu(F_EP, vo, ep + 1u);
     o7[0] = obs12[0]; o7[1] = obs12[1]; o7[2] = obs12[2];
 #pragma unroll
     for (int j = 0; j < 4; j++) { o7[3 + j] = 0.f; prev[j] = 0.f; }
   }
   store_env(p, i, e, false);
 #pragma unroll
-  for (int j = 0; j < 4; j++) p.soa[(F_PREV + j) * p.n + i] = prev[j];
+  for (int j = 0; j < 4; j++) S.st(F_PREV + j, vo, prev[j]);
 #pragma unroll
   for (int j = 0; j < 7; j++) out.obs[size_t(i) * 7 + j] = o7[j];
 }
@@ -270,8 +403,9 @@ __device__ __forceinline__ T grp_pick(int m, const T* v) {  // v[m], m lane-depe
 }
 
 template <int KIND, bool CTBR, int G>
-__global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __restrict__ act,
-                                                  QuadStepOut out) {
+__global__ __launch_bounds__(BLOCK) void k_step_g(const KConsts<float>* __restrict__ kc, KParams p,
+                                                  const float4* __restrict__ act, QuadStepOut out) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
   constexpr int NI = 4 / G;  // items per lane
   const unsigned i_raw = unsigned(p.first) + (blockIdx.x * BLOCK + threadIdx.x) / G;
   const int l = G == 1 ? 0 : int(threadIdx.x & (G - 1));
@@ -283,33 +417,33 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
   const unsigned i = live ? i_raw : end - 1;
   const KConsts<float>& k = *p.kc;
   const PhysConsts<float>& c = k.ph;
-  const size_t n = size_t(p.n);
-  const float* __restrict__ S = p.soa;
+  const Tiles S(p);
+  const uint32_t vo = env_off(i);
   // ---- load: shared fields by every lane; per-prop / per-axis fields by their owner lane
   float pos[3], q[4], v[3], w[3], tgt[3];
 #pragma unroll
   for (int j = 0; j < 3; j++) {
-    pos[j] = (S + (F_QPOS + j) * n)[i];
-    v[j] = (S + (F_QVEL + j) * n)[i];
-    w[j] = (S + (F_QVEL + 3 + j) * n)[i];
-    tgt[j] = (S + (F_TGT + j) * n)[i];
+    pos[j] = S.ld(F_QPOS + j, vo);
+    v[j] = S.ld(F_QVEL + j, vo);
+    w[j] = S.ld(F_QVEL + 3 + j, vo);
+    tgt[j] = S.ld(F_TGT + j, vo);
   }
 #pragma unroll
-  for (int j = 0; j < 4; j++) q[j] = (S + (F_QPOS + 3 + j) * n)[i];
-  float volt = (S + F_VOLT * n)[i];
-  int step = p.step[i];
-  const uint32_t ep = p.ep[i];  // prefetched: the reset branch must not add a dependent load
+  for (int j = 0; j < 4; j++) q[j] = S.ld(F_QPOS + 3 + j, vo);
+  float volt = S.ld(F_VOLT, vo);
+  int step = int(S.ldu(F_STEP, vo));
+  const uint32_t ep = S.ldu(F_EP, vo);  // prefetched: the reset branch must not add a dependent load
   float th[NI], sp[NI];
 #pragma unroll
   for (int it = 0; it < NI; it++) {
     const int pr = l + it * G;
-    th[it] = (S + (F_QPOS + 7 + pr) * n)[i];
-    sp[it] = (S + (F_QVEL + 6 + pr) * n)[i];
+    th[it] = G == 1 ? S.ld(F_QPOS + 7 + pr, vo) : S.ldv(F_QPOS + 7 + pr, vo);
+    sp[it] = G == 1 ? S.ld(F_QVEL + 6 + pr, vo) : S.ldv(F_QVEL + 6 + pr, vo);
   }
   float ri[3] = {0.f, 0.f, 0.f};
   if (CTBR) {
 #pragma unroll
-    for (int j = 0; j < 3; j++) ri[j] = (S + (F_RINT + j) * n)[i];
+    for (int j = 0; j < 3; j++) ri[j] = S.ld(F_RINT + j, vo);
   }
   const float4 a4 = act[i];
   float a[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -554,6 +688,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
     }
   };
   obs_triples(s12, tgt);
+  settle(ep);
   if (l == 0 && live) {
     out.reward[i] = reward;
     out.terminated[i] = term;
@@ -562,7 +697,9 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
     if (out.motor_commands)
       reinterpret_cast<float4*>(out.motor_commands)[i] = make_float4(float(F[0]), float(F[1]), float(F[2]), float(F[3]));
   }
-  if (out.state12 && live) {
+  if (G == 1 && out.state12 && live) {
+    store_row12(out.state12, i, s12);
+  } else if (out.state12 && live) {
 #pragma unroll
     for (int it = 0; it < NI; it++) {
       const int m = l + it * G;
@@ -573,7 +710,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
   }
   if (out.target_info && live && l == 0) {  // info target (+ spline velocity / acceleration)
     float o[9] = {tgt[0], tgt[1], tgt[2], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (KIND == QUAD_ENV_TRAJ) traj_spline_info(k, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, tgt, step, o);
+    if (KIND == QUAD_ENV_TRAJ) traj_spline_info(k, p.seed, p.gid_base + uint64_t(i), ep - 1u, tgt, step, o);
 #pragma unroll
     for (int j = 0; j < 9; j++) out.target_info[size_t(i) * 9 + j] = o[j];
   }
@@ -581,10 +718,16 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
   const bool reset = (term || trunc) && p.auto_reset;
   if (reset) {
     if (out.terminal_obs && live) {
+      if constexpr (G == 1) {
+        const float o12[12] = {ob[0][0], ob[0][1], ob[0][2], ob[1][0], ob[1][1], ob[1][2],
+                               ob[2][0], ob[2][1], ob[2][2], ob[3][0], ob[3][1], ob[3][2]};
+        store_row12(out.terminal_obs, i, o12);
+      } else {
 #pragma unroll
-      for (int it = 0; it < NI; it++)
+        for (int it = 0; it < NI; it++)
 #pragma unroll
-        for (int j = 0; j < 3; j++) out.terminal_obs[size_t(i) * 12 + 3 * (l + it * G) + j] = ob[it][j];
+          for (int j = 0; j < 3; j++) out.terminal_obs[size_t(i) * 12 + 3 * (l + it * G) + j] = ob[it][j];
+      }
     }
     const uint64_t gid = p.gid_base + uint64_t(i);
     uint32_t r[NI][4];
@@ -641,7 +784,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
     volt = float(k.vnom);
     step = 0;
     obs_triples(init12, tgt);  // QuadState round trip of the drawn state == the draw itself
-    if (l == 0 && live) p.ep[i] = ep + 1;
+    if (l == 0 && live) S.stu(F_EP, vo, ep + 1u);
   }
   // ---- stores: obs rows. G = 1: staged through LDS so every wave-store writes 1 KiB
   // contiguously; G > 1: one dwordx3 per lane, a wave's rows are already contiguous.
@@ -658,26 +801,30 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(KParams p, const float4* __res
     }
   }
   if (!live) return;
-  float* __restrict__ Sw = p.soa;
 #pragma unroll
   for (int it = 0; it < NI; it++) {
     const int pr = l + it * G;
-    (Sw + (F_QPOS + 7 + pr) * n)[i] = th[it];
-    (Sw + (F_QVEL + 6 + pr) * n)[i] = sp[it];
+    if (G == 1) {
+      S.st(F_QPOS + 7 + pr, vo, th[it]);
+      S.st(F_QVEL + 6 + pr, vo, sp[it]);
+    } else {
+      S.stv(F_QPOS + 7 + pr, vo, th[it]);
+      S.stv(F_QVEL + 6 + pr, vo, sp[it]);
+    }
   }
   if (l == 0) {
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-      (Sw + (F_QPOS + j) * n)[i] = pos[j];
-      (Sw + (F_QVEL + j) * n)[i] = v[j];
-      (Sw + (F_QVEL + 3 + j) * n)[i] = w[j];
-      if (reset) (Sw + (F_TGT + j) * n)[i] = tgt[j];  // the target only changes on reset
-      if (CTBR) (Sw + (F_RINT + j) * n)[i] = ri[j];
+      S.st(F_QPOS + j, vo, pos[j]);
+      S.st(F_QVEL + j, vo, v[j]);
+      S.st(F_QVEL + 3 + j, vo, w[j]);
+      if (reset) S.st(F_TGT + j, vo, tgt[j]);  // the target only changes on reset
+      if (CTBR) S.st(F_RINT + j, vo, ri[j]);
     }
 #pragma unroll
-    for (int j = 0; j < 4; j++) (Sw + (F_QPOS + 3 + j) * n)[i] = q[j];
-    (Sw + F_VOLT * n)[i] = volt;
-    p.step[i] = step;
+    for (int j = 0; j < 4; j++) S.st(F_QPOS + 3 + j, vo, q[j]);
+    S.st(F_VOLT, vo, volt);
+    S.stu(F_STEP, vo, uint32_t(step));
   }
 }
 
@@ -689,10 +836,14 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KParams p, const uint8_t* __res
   if (mask && !mask[i]) return;
   EnvRegs<float> e;
   float obs[12];
-  reset_env<KIND>(p, i, e, obs);
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
+  const uint32_t ep = S.ldu(F_EP, vo);
+  reset_env<KIND>(p, i, e, obs, ep);
+  S.stu(F_EP, vo, ep + 1u);
   store_env(p, i, e, true);
 #pragma unroll
-  for (int j = 0; j < 4; j++) p.soa[(F_PREV + j) * p.n + i] = 0.f;  // hover_env.py:212
+  for (int j = 0; j < 4; j++) S.st(F_PREV + j, vo, 0.f);  // hover_env.py:212
   if (obs_out) {
     if (RELPOS) {
 #pragma unroll
@@ -709,8 +860,9 @@ __global__ __launch_bounds__(BLOCK) void k_reset(KParams p, const uint8_t* __res
 // AutoResetWrapper: the env returns to the FIRST state of its episode -- regenerated from the draw
 // of the last explicit reset (episode counter - 1) instead of being stored.
 template <int KIND>
-__global__ __launch_bounds__(BLOCK) void k_step_brax(KParams p, const float4* __restrict__ act,
-                                                     QuadStepOut out) {
+__global__ __launch_bounds__(BLOCK) void k_step_brax(const KConsts<float>* __restrict__ kc, KParams p,
+                                                     const float4* __restrict__ act, QuadStepOut out) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
   const int i = p.first + blockIdx.x * BLOCK + threadIdx.x;
   if (i >= p.first + p.count) return;
   EnvRegs<float> e;
@@ -736,7 +888,8 @@ __global__ __launch_bounds__(BLOCK) void k_step_brax(KParams p, const float4* __
       for (int j = 0; j < 21; j++) out.terminal_obs[size_t(i) * 21 + j] = obs[j];
     }
     float u21[21];
-    brax_reset_draw(p.kc->bx_noise, p.seed, p.gid_base + uint64_t(i), p.ep[i] - 1u, u21);
+    brax_reset_draw(p.kc->bx_noise, p.seed, p.gid_base + uint64_t(i),
+                    Tiles(p).ldu(F_EP, env_off(uint32_t(i))) - 1u, u21);
     brax_reset_from<float, KIND>(*p.kc, e, u21, obs, true);
   }
   store_env(p, i, e, true);
@@ -750,12 +903,14 @@ __global__ __launch_bounds__(BLOCK) void k_reset_brax(KParams p, const uint8_t* 
   const int i = blockIdx.x * BLOCK + threadIdx.x;
   if (i >= p.n) return;
   if (mask && !mask[i]) return;
-  const uint32_t ep = p.ep[i];
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
+  const uint32_t ep = S.ldu(F_EP, vo);
   float u21[21], obs[21];
   brax_reset_draw(p.kc->bx_noise, p.seed, p.gid_base + uint64_t(i), ep, u21);
   EnvRegs<float> e;
   brax_reset_from<float, KIND>(*p.kc, e, u21, obs, false);
-  p.ep[i] = ep + 1u;
+  S.stu(F_EP, vo, ep + 1u);
   store_env(p, i, e, true);
   if (obs_out) {
 #pragma unroll
@@ -766,9 +921,10 @@ __global__ __launch_bounds__(BLOCK) void k_reset_brax(KParams p, const uint8_t* 
 __global__ __launch_bounds__(BLOCK) void k_observe_brax(KParams p, float* __restrict__ obs_out) {
   const int i = blockIdx.x * BLOCK + threadIdx.x;
   if (i >= p.n) return;
-  const float* s = p.soa;
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
 #pragma unroll
-  for (int j = 0; j < 21; j++) obs_out[size_t(i) * 21 + j] = s[(F_QPOS + j) * p.n + i];  // qpos, qvel
+  for (int j = 0; j < 21; j++) obs_out[size_t(i) * 21 + j] = S.ld(F_QPOS + j, vo);  // qpos, qvel
 }
 
 template <bool RELPOS>
@@ -783,7 +939,7 @@ __global__ __launch_bounds__(BLOCK) void k_observe(KParams p, float* __restrict_
   if (RELPOS) {
 #pragma unroll
     for (int j = 0; j < 7; j++)
-      obs_out[size_t(i) * 7 + j] = j < 3 ? obs[j] : p.soa[(F_PREV + j - 3) * p.n + i];
+      obs_out[size_t(i) * 7 + j] = j < 3 ? obs[j] : Tiles(p).ld(F_PREV + j - 3, env_off(uint32_t(i)));
   } else {
 #pragma unroll
     for (int j = 0; j < 12; j++) obs_out[size_t(i) * 12 + j] = obs[j];
@@ -805,21 +961,21 @@ __global__ __launch_bounds__(BLOCK) void k_waypoints_begin(KParams p, QuadWaypoi
   const int cnt = w.counts[set];
   const double* wp = w.points + size_t(set) * w.max_points * 3;
   const int nxt = 1 % cnt;
-  const int n = p.n;
-  float* S = p.soa;
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
 #pragma unroll
   for (int j = 0; j < 3; j++) {
-    S[(F_QPOS + j) * n + i] = float(wp[j]);
-    S[(F_QVEL + j) * n + i] = 0.f;
-    S[(F_QVEL + 3 + j) * n + i] = 0.f;
-    S[(F_TGT + j) * n + i] = float(wp[3 * nxt + j]);  // waypoints[i].astype(np.float32)
-    S[(F_RINT + j) * n + i] = 0.f;
+    S.st(F_QPOS + j, vo, float(wp[j]));
+    S.st(F_QVEL + j, vo, 0.f);
+    S.st(F_QVEL + 3 + j, vo, 0.f);
+    S.st(F_TGT + j, vo, float(wp[3 * nxt + j]));  // waypoints[i].astype(np.float32)
+    S.st(F_RINT + j, vo, 0.f);
   }
-  S[(F_QPOS + 3) * n + i] = 1.f;
-  S[(F_QPOS + 4) * n + i] = 0.f;
-  S[(F_QPOS + 5) * n + i] = 0.f;
-  S[(F_QPOS + 6) * n + i] = 0.f;
-  p.step[i] = 0;
+  S.st(F_QPOS + 3, vo, 1.f);
+  S.st(F_QPOS + 4, vo, 0.f);
+  S.st(F_QPOS + 5, vo, 0.f);
+  S.st(F_QPOS + 6, vo, 0.f);
+  S.stu(F_STEP, vo, 0u);
   t.wp_idx[i] = nxt;
   t.reached[i] = 0;
   t.laps[i] = 0;
@@ -832,7 +988,7 @@ __global__ __launch_bounds__(BLOCK) void k_waypoints_begin(KParams p, QuadWaypoi
   observe(*p.kc, e, obs, s12);
   if (RELPOS) {
 #pragma unroll
-    for (int j = 0; j < 7; j++) obs_out[size_t(i) * 7 + j] = j < 3 ? obs[j] : S[(F_PREV + j - 3) * n + i];
+    for (int j = 0; j < 7; j++) obs_out[size_t(i) * 7 + j] = j < 3 ? obs[j] : S.ld(F_PREV + j - 3, vo);
   } else {
 #pragma unroll
     for (int j = 0; j < 12; j++) obs_out[size_t(i) * 12 + j] = obs[j];
@@ -870,12 +1026,40 @@ __global__ __launch_bounds__(BLOCK) void k_waypoints_update(KParams p, QuadWaypo
       status = 1;
     } else {
 #pragma unroll
-      for (int j = 0; j < 3; j++) p.soa[(F_TGT + j) * p.n + i] = float(wp[3 * k + j]);
+      for (int j = 0; j < 3; j++) Tiles(p).st(F_TGT + j, env_off(uint32_t(i)), float(wp[3 * k + j]));
     }
   }
   if (status == 0 && term[i]) status = 2;
   else if (status == 0 && trunc[i]) status = 3;
   t.status[i] = status;
+}
+
+// quad_get_state / quad_set_state: the dense [fields][N] pieces of QuadStateSoA <-> the tiles
+struct StateIO {
+  uint32_t* ptr[8];  // device pointers (4-byte elements), NULL = piece skipped
+  int32_t f0[8], cnt[8];
+};
+template <bool TO_TILES>
+__global__ __launch_bounds__(BLOCK) void k_state_io(KParams p, StateIO u) {
+  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= p.n) return;
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
+  const size_t n = size_t(p.n);
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    if (!u.ptr[k]) continue;
+    for (int j = 0; j < u.cnt[k]; j++) {  // f uniform: the SGPR part of the offset stays scalar
+      uint32_t* d = u.ptr[k] + size_t(j) * n + i;
+      if (TO_TILES) S.stu(u.f0[k] + j, vo, *d);
+      else *d = S.ldu(u.f0[k] + j, vo);
+    }
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_fill_field(KParams p, int32_t f, uint32_t x) {
+  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i < p.n) Tiles(p).stu(f, env_off(uint32_t(i)), x);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_random_actions(int32_t n, uint64_t seed, uint64_t gid_base,
@@ -922,9 +1106,9 @@ struct QuadHandle {
   KParams kp;
   int device;
   int n;
-  float* soa = nullptr;
-  int32_t* step = nullptr;
-  uint32_t* ep = nullptr;
+  float* tiles = nullptr;     // env state (layout at the top of this file)
+  size_t tile_bytes = 0;
+  uint32_t* stage = nullptr;  // [NFT][n] staging for host-side get/set_state, allocated on first use
   KConsts<float> kh;                 // host copy of the constant block
   KConsts<float>* kdev = nullptr;    // device copy the kernels read (scalar loads, K$-resident)
 };
@@ -1031,8 +1215,9 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   if (!cfg || !out) return fail(QUAD_EINVAL, "cfg/out is NULL");
   *out = nullptr;
   if (n_envs <= 0) return fail(QUAD_EINVAL, "n_envs must be > 0");
-  if (int64_t(n_envs) * NF > int64_t(INT32_MAX) || int64_t(n_envs) * 4 > int64_t(INT32_MAX))
-    return fail(QUAD_EINVAL, "n_envs too large");
+  // the tiles are one buffer resource (32-bit byte range); row outputs use 32-bit byte offsets
+  if ((int64_t(n_envs) + 63) / 64 * TILE_BYTES > int64_t(UINT32_MAX))
+    return fail(QUAD_EINVAL, "n_envs too large (max 31,580,608)");
   if (cfg->env_kind < QUAD_ENV_HOVER || cfg->env_kind > QUAD_ENV_BRAX_TRAJ)
     return fail(QUAD_EINVAL, "unknown env_kind");
   if (cfg->wrapper < QUAD_WRAP_NONE || cfg->wrapper > QUAD_WRAP_RELPOS)
@@ -1055,12 +1240,9 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   h->device = device;
   h->n = n_envs;
   DeviceGuard g(device);
-  hipError_t e = hipMalloc(&h->soa, sizeof(float) * size_t(NF) * n_envs);
-  if (e == hipSuccess) e = hipMalloc(&h->step, sizeof(int32_t) * size_t(n_envs));
-  if (e == hipSuccess) e = hipMalloc(&h->ep, sizeof(uint32_t) * size_t(n_envs));
-  if (e == hipSuccess) e = hipMemset(h->soa, 0, sizeof(float) * size_t(NF) * n_envs);
-  if (e == hipSuccess) e = hipMemset(h->step, 0, sizeof(int32_t) * size_t(n_envs));
-  if (e == hipSuccess) e = hipMemset(h->ep, 0, sizeof(uint32_t) * size_t(n_envs));
+  h->tile_bytes = size_t((n_envs + 63) / 64) * TILE_BYTES;
+  hipError_t e = hipMalloc(&h->tiles, h->tile_bytes);
+  if (e == hipSuccess) e = hipMemset(h->tiles, 0, h->tile_bytes);
   if (e == hipSuccess) e = hipMalloc(&h->kdev, sizeof(KConsts<float>));
   if (e == hipSuccess) e = hipMemcpy(h->kdev, &h->kh, sizeof(KConsts<float>), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -1069,9 +1251,8 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
     return hip_fail(e, "quad_create allocation");
   }
   h->kp.kc = h->kdev;
-  h->kp.soa = h->soa;
-  h->kp.step = h->step;
-  h->kp.ep = h->ep;
+  h->kp.tiles = h->tiles;
+  h->kp.tile_bytes = uint32_t(h->tile_bytes);
   h->kp.n = n_envs;
   h->kp.first = 0;
   h->kp.count = n_envs;
@@ -1092,9 +1273,8 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
 void quad_destroy(QuadHandle* h) {
   if (!h) return;
   DeviceGuard g(h->device);
-  if (h->soa) (void)hipFree(h->soa);
-  if (h->step) (void)hipFree(h->step);
-  if (h->ep) (void)hipFree(h->ep);
+  if (h->tiles) (void)hipFree(h->tiles);
+  if (h->stage) (void)hipFree(h->stage);
   if (h->kdev) (void)hipFree(h->kdev);
   delete h;
 }
@@ -1105,7 +1285,9 @@ int quad_seed(QuadHandle* h, uint64_t seed, void* stream) {
   if (!h) return fail(QUAD_EINVAL, "handle is NULL");
   DeviceGuard g(h->device);
   h->kp.seed = seed;
-  HIP_TRY(hipMemsetAsync(h->ep, 0, sizeof(uint32_t) * size_t(h->n), static_cast<hipStream_t>(stream)));
+  hipLaunchKernelGGL(k_fill_field, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
+                     h->kp, int32_t(F_EP), 0u);
+  HIP_TRY(hipGetLastError());
   return QUAD_OK;
 }
 
@@ -1157,36 +1339,36 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
   if (h->cfg.wrapper == QUAD_WRAP_RELPOS) {
     const dim3 grid(grid_of(count));
     if (traj)
-      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_TRAJ>), grid, blk, 0, s, kp, a, *out);
+      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_TRAJ>), grid, blk, 0, s, h->kdev, kp, a, *out);
     else
-      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_HOVER>), grid, blk, 0, s, kp, a, *out);
+      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_HOVER>), grid, blk, 0, s, h->kdev, kp, a, *out);
   } else if (h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) {
     const dim3 grid(grid_of(count));
     if (h->cfg.env_kind == QUAD_ENV_BRAX_TRAJ)
-      hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_TRAJ>), grid, blk, 0, s, kp, a, *out);
+      hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_TRAJ>), grid, blk, 0, s, h->kdev, kp, a, *out);
     else
-      hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_HOVER>), grid, blk, 0, s, kp, a, *out);
+      hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_HOVER>), grid, blk, 0, s, h->kdev, kp, a, *out);
   } else if (G == 0) {  // legacy one-thread-per-env form with the LDS obs transpose (A/B reference)
     const dim3 grid(grid_of(count));
     if (traj && ctbr)
-      hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, kp, a, *out);
+      hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, h->kdev, kp, a, *out);
     else if (traj)
-      hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false>), grid, blk, 0, s, kp, a, *out);
+      hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false>), grid, blk, 0, s, h->kdev, kp, a, *out);
     else if (ctbr)
-      hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true>), grid, blk, 0, s, kp, a, *out);
+      hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true>), grid, blk, 0, s, h->kdev, kp, a, *out);
     else
-      hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false>), grid, blk, 0, s, kp, a, *out);
+      hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false>), grid, blk, 0, s, h->kdev, kp, a, *out);
   } else {
     const dim3 grid(unsigned((int64_t(count) * G + BLOCK - 1) / BLOCK));
 #define QD_LAUNCH(GG)                                                                              \
   if (traj && ctbr)                                                                             \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, true, GG>), grid, blk, 0, s, kp, a, *out);   \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, true, GG>), grid, blk, 0, s, h->kdev, kp, a, *out);   \
   else if (traj)                                                                                \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, false, GG>), grid, blk, 0, s, kp, a, *out);  \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, false, GG>), grid, blk, 0, s, h->kdev, kp, a, *out);  \
   else if (ctbr)                                                                                \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, true, GG>), grid, blk, 0, s, kp, a, *out);  \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, true, GG>), grid, blk, 0, s, h->kdev, kp, a, *out);  \
   else                                                                                          \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG>), grid, blk, 0, s, kp, a, *out);
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG>), grid, blk, 0, s, h->kdev, kp, a, *out);
     if (G == 1) { QD_LAUNCH(1) } else if (G == 2) { QD_LAUNCH(2) } else { QD_LAUNCH(4) }
 #undef QD_LAUNCH
   }
@@ -1230,25 +1412,32 @@ static int copy_state(QuadHandle* h, const QuadStateSoA* u, int on_host, void* s
   DeviceGuard g(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
   const size_t n = size_t(h->n);
-  const hipMemcpyKind kind = on_host ? (to_handle ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost)
-                                     : hipMemcpyDeviceToDevice;
-  struct Piece { void* user; void* mine; size_t bytes; };
+  struct Piece { void* user; int f0, cnt; };  // user: dense [cnt][n] 4-byte elements
   const Piece pieces[8] = {
-      {u->qpos, h->soa + F_QPOS * n, 11 * n * sizeof(float)},
-      {u->qvel, h->soa + F_QVEL * n, 10 * n * sizeof(float)},
-      {u->voltage, h->soa + F_VOLT * n, n * sizeof(float)},
-      {u->target, h->soa + F_TGT * n, 3 * n * sizeof(float)},
-      {u->rate_int, h->soa + F_RINT * n, 3 * n * sizeof(float)},
-      {u->step_count, h->step, n * sizeof(int32_t)},
-      {u->episode, h->ep, n * sizeof(uint32_t)},
-      {u->prev_action, h->soa + F_PREV * n, 4 * n * sizeof(float)},
+      {u->qpos, F_QPOS, 11}, {u->qvel, F_QVEL, 10}, {u->voltage, F_VOLT, 1}, {u->target, F_TGT, 3},
+      {u->rate_int, F_RINT, 3}, {u->step_count, F_STEP, 1}, {u->episode, F_EP, 1}, {u->prev_action, F_PREV, 4},
   };
-  for (const Piece& p : pieces) {
-    if (!p.user) continue;
-    if (to_handle)
-      HIP_TRY(hipMemcpyAsync(p.mine, p.user, p.bytes, kind, s));
-    else
-      HIP_TRY(hipMemcpyAsync(p.user, p.mine, p.bytes, kind, s));
+  if (on_host && !h->stage) HIP_TRY(hipMalloc(&h->stage, sizeof(uint32_t) * size_t(NFT) * n));
+  StateIO io;
+  for (int k = 0; k < 8; k++) {
+    const Piece& p = pieces[k];
+    io.f0[k] = p.f0;
+    io.cnt[k] = p.cnt;
+    io.ptr[k] = !p.user ? nullptr : on_host ? h->stage + size_t(p.f0) * n : static_cast<uint32_t*>(p.user);
+  }
+  const size_t esz = sizeof(uint32_t);
+  if (to_handle) {
+    if (on_host)
+      for (const Piece& p : pieces)
+        if (p.user) HIP_TRY(hipMemcpyAsync(h->stage + size_t(p.f0) * n, p.user, esz * p.cnt * n, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_state_io<true>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, io);
+    HIP_TRY(hipGetLastError());
+  } else {
+    hipLaunchKernelGGL(k_state_io<false>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, io);
+    HIP_TRY(hipGetLastError());
+    if (on_host)
+      for (const Piece& p : pieces)
+        if (p.user) HIP_TRY(hipMemcpyAsync(p.user, h->stage + size_t(p.f0) * n, esz * p.cnt * n, hipMemcpyDeviceToHost, s));
   }
   if (on_host) HIP_TRY(hipStreamSynchronize(s));
   return QUAD_OK;
