@@ -68,6 +68,11 @@ int hip_fail(hipError_t e, const char* what) {
     if (e__ != hipSuccess) return hip_fail(e__, #expr); \
   } while (0)
 
+// The step kernels take the constant block as a separate `const KConsts<float>* __restrict__`
+// argument and copy it into p.kc: the argument's noalias lets the compiler keep every constant read
+// a scalar load even after the kernel's first global store. Read through a plain struct member it
+// could not rule out a clobber, and constants read after a store became VMEM loads whose vmcnt
+// waits (gfx9 counts stores too) drained the stores already issued.
 struct KParams {
   const KConsts<float>* __restrict__ kc;  // per-handle constant block in device memory
   float* tiles;         // env state tiles (layout above)
@@ -170,10 +175,8 @@ __device__ __forceinline__ void store_env(const KParams& p, int i, const EnvRegs
   S.stu(F_STEP, o, uint32_t(e.step));
 }
 
-// The reset draw of episode `ep` (the env's counter, loaded by the caller with the state); the
-// caller stores ep + 1 after its other stores. Step kernels issue every global store after this:
-// a store ahead of the constant-block reads would make them VMEM loads (the compiler can no
-// longer rule out a clobber), each with a vmcnt wait that on gfx9 also drains the stores.
+// The reset draw of episode `ep` (the env's counter, loaded by the caller with the state; the
+// caller stores ep + 1).
 template <int KIND>
 __device__ __forceinline__ void reset_env(const KParams& p, int i, EnvRegs<float>& e, float obs[12],
                                           uint32_t ep) {
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_relpos(const KConsts<float>* __r
   const bool rs = (r.term || r.trunc) && p.auto_reset;
   float obs12[12];
   if (rs) reset_env<KIND>(p, i, e, obs12, ep);
-  // ---- every global store after the reset (see reset_env)
+  // ---- outputs (k_step_relpos keeps them after the reset: its 7-wide rows need o7 either way)
   out.reward[i] = r.reward;
   out.terminated[i] = r.term;
   out.truncated[i] = r.trunc;
