@@ -207,39 +207,63 @@ def _end_to_end(env, args) -> dict:
 
 
 def _rollout_phase(env, args) -> dict:
-    """PPO rollout phase on the same 65,536 envs, one hipGraph per rollout step, GAE included,
-    timed over n_steps: the MFMA policy path (policy kernel + env step + epilogue = 3 launches)
-    and, for comparison, the same step as torch ops on the same policy."""
+    """PPO rollout phase on the same 65,536 envs, timed over n_steps, GAE included, three ways:
+    the one-launch rollout (quad_rollout: policy + env step + bootstrap + statistics for all steps
+    in one kernel, the PPO default), the two-launch MFMA path (policy kernel + env step per step,
+    graph-replayed) and the same step as torch ops on the same policy."""
     from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
     out = {"n_steps": args.rollout_steps,
            "what": "actor+critic MLP 12-128-128 fp32 + Gaussian sample + clip + env step + "
-                   "TimeLimit bootstrap + buffer rows, graph-replayed; GAE included"}
-    for name, fused in (("mfma", True), ("torch", False)):
-        m = PPO(env, PPOConfig(n_steps=args.rollout_steps, fused_policy=fused), seed=0)
+                   "TimeLimit bootstrap + buffer rows; GAE included"}
+    n = env.num_envs
+    flop_step = n * (2 * 2 * (12 * 128 + 128 * 128) + 2 * 128 * 5)  # both nets + heads, per env-step
+    for name, fused, one in (("one_launch", True, True), ("mfma", True, False), ("torch", False, False)):
+        m = PPO(env, PPOConfig(n_steps=args.rollout_steps, fused_policy=fused, fused_rollout=one), seed=0)
         m.collect_rollouts(use_graph=True)  # capture + warm
         rs = m.collect_rollouts(use_graph=True)
         out[name] = {"env_steps_per_s": rs.env_steps / rs.seconds,
                      "ms_per_step": rs.seconds / args.rollout_steps * 1e3}
-        if fused:  # the policy kernel alone (HIP events on its stream): MFMA roofline
-            n = env.num_envs
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if one:  # the rollout kernel alone: HIP events on its stream, one launch = n_steps steps
+            def launch():
+                m._fp.rollout(env, obs_copy=m.buf_obs, actions=m.buf_act, log_prob=m.buf_logp,
+                              value=m.buf_val, episode_starts=m.buf_start, rewards=m.buf_rew,
+                              last_obs=m.last_obs, last_start=m.last_start, ep_ret=m.ep_ret,
+                              ep_len=m.ep_len, stats=m._slots, t0=0, steps=args.rollout_steps,
+                              seed=1, gamma=m.cfg.gamma)
+            launch()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(3):
+                launch()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / 3
+            flop = flop_step * args.rollout_steps
+            out["rollout_kernel"] = {
+                "kernel": "k_rollout<HOVER,noCTBR>", "steps_per_launch": args.rollout_steps,
+                "kernel_us": us, "us_per_step": us / args.rollout_steps,
+                "env_steps_per_s": n * args.rollout_steps / (us * 1e-6),
+                "flop_per_launch": flop, "achieved_TFLOPs": flop / (us * 1e-6) / 1e12,
+                "peak_TFLOPs": 157.3, "bound": "mfma (fp32 32x32x2)"}
+        elif fused:  # the two-launch path's policy kernel alone: MFMA roofline
             ae = torch.empty(n, 4, device=env.device)
             for _ in range(5):
                 m._fp.act(m.last_obs, ae, seed=1)
             torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(100):
                 m._fp.act(m.last_obs, ae, seed=1)
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / 100
-            flop = n * (2 * 2 * (12 * 128 + 128 * 128) + 2 * 128 * 5)
             out["policy_kernel"] = {"kernel": "k_policy_act<2,256>", "kernel_us": us,
-                                    "flop_per_launch": flop, "achieved_TFLOPs": flop / (us * 1e-6) / 1e12,
+                                    "flop_per_launch": flop_step,
+                                    "achieved_TFLOPs": flop_step / (us * 1e-6) / 1e12,
                                     "peak_TFLOPs": 157.3, "bound": "mfma (fp32 32x32x2)"}
         del m
         torch.cuda.empty_cache()
-    out["env_steps_per_s"] = out["mfma"]["env_steps_per_s"]
+    out["env_steps_per_s"] = out["one_launch"]["env_steps_per_s"]
     return out
 
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define QUADENV_ABI_VERSION 2
+#define QUADENV_ABI_VERSION 3
 
 enum { QUAD_OK = 0, QUAD_EINVAL = -1, QUAD_EHIP = -2, QUAD_ENOMEM = -3, QUAD_EMODEL = -4 };
 /* QUAD_ENV_BRAX_HOVER / QUAD_ENV_BRAX_TRAJ: the brax Env API siblings of the same path
@@ -286,6 +286,39 @@ int quad_policy_act(const float* packed, const QuadPolicyAct* a, int32_t n, void
  * marks one pending, then clears the mark. A no-op otherwise. */
 int quad_rollout_post(const float* packed, const QuadRolloutPost* p, uint32_t* cursor, int32_t n,
                       void* stream);
+
+/* ---- Fused rollout: `steps` whole steps of SB3 OnPolicyAlgorithm.collect_rollouts (train.py:50-68
+ * drives it through SB3's PPO.learn) in ONE launch -- per step: policy (both MLPs on MFMA,
+ * Gaussian sample, log-prob, clip), the env step of the handle (HoverEnv / TrajectoryFollowEnv,
+ * optional RateControlWrapper, SB3 auto-reset), TimeLimit bootstrap, Monitor statistics, buffer
+ * rows. Each 256-env block keeps its envs' state in registers and the packed weights in LDS for
+ * all `steps`, so per step nothing is read from HBM. Results are bit-identical to the two-launch
+ * form (quad_policy_act with epilogue + quad_step, then quad_rollout_post) with cursor t = t0.
+ * Requires: a handle with env_kind HOVER or TRAJ, wrapper NONE or CTBR, auto_reset = 1.
+ * Step t (t0 <= t < t0 + steps) writes row t % rows of the time-major buffers (every row pointer
+ * required) and draws its action noise from Philox(seed; env_id_base + env, t, 0x200).
+ * last_obs / last_start / ep_ret / ep_len carry the rollout across calls (read at entry, written
+ * at exit); stats[slot] accumulate (finished return, length, count) as in QuadRolloutPost. */
+typedef struct QuadRollout {
+  float* obs_copy;          /* [rows,N,12] observation the step's action was taken from */
+  float* actions;           /* [rows,N,4] unclipped sample (16-byte aligned) */
+  float* log_prob;          /* [rows,N] */
+  float* value;             /* [rows,N] V(obs) */
+  float* episode_starts;    /* [rows,N] */
+  float* rewards;           /* [rows,N] reward (+ gamma V(terminal_obs) on time-limit truncation) */
+  float* last_obs;          /* [N,12] in: obs of step t0; out: obs after the last step */
+  float* last_start;        /* [N] in/out: 1.0 where the next step begins an episode */
+  float* ep_ret;            /* [N] in/out: running episode return */
+  float* ep_len;            /* [N] in/out: running episode length */
+  double* stats;            /* [QUAD_POLICY_STAT_SLOTS][3], accumulated */
+  int32_t rows;             /* >= 1 */
+  int32_t t0;               /* >= 0 */
+  int32_t steps;            /* >= 1 */
+  int32_t deterministic;    /* 1: a = mean */
+  uint64_t seed;            /* action-noise seed */
+  float gamma;
+} QuadRollout;
+int quad_rollout(QuadHandle* h, const float* packed, const QuadRollout* r, void* stream);
 
 #ifdef __cplusplus
 }

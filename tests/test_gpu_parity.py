@@ -424,6 +424,26 @@ def test_ragged_sizes_match_oracle(n, kernel_variant):
     env.close()
 
 
+@pytest.mark.parametrize("n", [1000, 4096 + 37])
+def test_ragged_mass_auto_reset_draws(n, kernel_variant):
+    """Every env truncates at once (max_episode_steps = 1) in a batch whose last wave is partly
+    empty: k_step computes the reset draws of a wave's resetting envs across ALL its lanes
+    (reset_words_wave), so lanes past N must take part. Each reset obs equals the oracle's draw."""
+    env = _env(n, seed=31, env_id_base=77, max_episode_steps=1)
+    env.reset()
+    cfg = O.default_cfg(O.ENV_HOVER, O.WRAP_NONE)
+    for k in range(2):
+        pre = env.get_state()
+        obs, rew, te, tr, inf = env.step(torch.zeros(n, 4, device="cuda"))
+        torch.cuda.synchronize()
+        assert bool(tr.all())
+        obs = obs.cpu().numpy()
+        for i in list(range(0, n, 97)) + list(range(n - 70, n)):
+            i12, t3 = O.reset_draw(cfg, 31, 77 + i, int(pre["episode"][i]))
+            assert np.array_equal(obs[i], O.Env(cfg=cfg).reset_with(i12, t3)), (k, i)
+    env.close()
+
+
 def test_four_million_envs_properties():
     """A 4,194,304-env batch (index arithmetic far past 2^16 blocks): every row finite, rewards in
     (0, 1], flags consistent with the state bounds, a strided oracle sample exact."""

@@ -1,0 +1,160 @@
+"""The one-launch rollout (quad_rollout, csrc/rollout.hip) against the two-launch form it fuses.
+
+The two-launch form -- k_policy_act with the fused epilogue, then quad_step, then
+quad_rollout_post -- is the path the rest of the GPU suite pins: its env step against the float64
+oracle (test_gpu_parity.py), its policy against the torch fp32 ActorCritic and its noise against the
+oracle's Philox + Box-Muller (test_gpu_policy.py). quad_rollout runs the same operations in one
+launch per chunk of steps with the env state in registers, so every buffer row, the carried
+last_obs / last_start / ep_ret / ep_len and the env state must agree BIT FOR BIT; the Monitor
+statistics are summed in a different order (float64 per thread vs float per block) and agree to
+1e-6 relative.
+
+Cases: hover / hover + RateControlWrapper / TrajectoryFollowEnv + RateControlWrapper; short
+max_episode_steps so that time-limit truncations (the critic bootstrap) occur besides
+terminations; ragged N (dead lanes in the last block); rollouts split over several launches.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _policy(seed=0):
+    from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
+    torch.manual_seed(seed)
+    pol = ActorCritic(12, 4, (128, 128)).cuda()
+    with torch.no_grad():  # small weights + small std: episodes survive long enough to truncate
+        for p in pol.parameters():
+            p.copy_(torch.randn_like(p) * (0.3 / math.sqrt(max(p.shape[-1], 1))))
+        pol.log_std.copy_(torch.tensor([-1.5, -2.0, -2.0, -2.5]))
+    return pol
+
+
+def _env(n, kind, wrapper, max_steps, seed=5, base=0):
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    env = QuadVecEnv(n, env=kind, wrapper=wrapper, device="cuda:0", seed=seed, env_id_base=base,
+                     max_episode_steps=max_steps)
+    return env
+
+
+def _bufs(T, n):
+    f = dict(dtype=torch.float32, device="cuda")
+    from uav_reinforcement_learning_control_amd import _native as N
+    return dict(obs_copy=torch.full((T, n, 12), -7.0, **f), actions=torch.full((T, n, 4), -7.0, **f),
+                log_prob=torch.full((T, n), -7.0, **f), value=torch.full((T, n), -7.0, **f),
+                episode_starts=torch.full((T, n), -7.0, **f), rewards=torch.full((T, n), -7.0, **f),
+                last_obs=torch.zeros(n, 12, **f), last_start=torch.ones(n, **f),
+                ep_ret=torch.zeros(n, **f), ep_len=torch.zeros(n, **f),
+                stats=torch.zeros(N.POLICY_STAT_SLOTS, 3, dtype=torch.float64, device="cuda"))
+
+
+def _two_launch(fp, env, b, T, seed, gamma):
+    cur = torch.zeros(4, dtype=torch.int32, device="cuda")
+    act_env = torch.zeros(env.num_envs, 4, device="cuda")
+    epi = fp.make_epilogue(env.reward, env.terminated, env.truncated, env.terminal_obs, b["rewards"],
+                           b["last_start"], b["ep_ret"], b["ep_len"], b["stats"], T, gamma)
+    for _ in range(T):
+        fp.act(b["last_obs"], act_env, actions=b["actions"], log_prob=b["log_prob"], value=b["value"],
+               obs_copy=b["obs_copy"], last_start=b["last_start"], episode_starts=b["episode_starts"],
+               cursor=cur, rows=T, seed=seed, env_id_base=env.env_id_base, epilogue=epi)
+        env.step(act_env, obs=b["last_obs"], info="raw")
+    fp.post(epi, cur)
+    torch.cuda.synchronize()
+
+
+def _one_launch(fp, env, b, T, seed, gamma, chunks):
+    t = 0
+    for k in chunks:
+        fp.rollout(env, t0=t, steps=k, seed=seed, gamma=gamma, **b)
+        t += k
+    assert t == T
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("kind,wrapper,max_steps,n,chunks", [
+    ("hover", None, 6, 1000, (20,)),
+    ("hover", "RateControlWrapper", 9, 4096 + 37, (7, 13)),
+    ("trajectory", "RateControlWrapper", 11, 777, (5, 5, 10)),
+    ("hover", None, 512, 65536, (20,)),
+])
+def test_one_launch_rollout_is_bit_identical(kind, wrapper, max_steps, n, chunks):
+    from uav_reinforcement_learning_control_amd.ppo.fused import FusedPolicy
+    T, seed, gamma = sum(chunks), 0x1234_5678_9ABC, 0.97
+    fp = FusedPolicy(_policy())
+    fp.pack()
+    ea, eb = _env(n, kind, wrapper, max_steps, base=3 * n), _env(n, kind, wrapper, max_steps, base=3 * n)
+    A, B = _bufs(T, n), _bufs(T, n)
+    A["last_obs"].copy_(ea.reset())
+    B["last_obs"].copy_(eb.reset())
+    _two_launch(fp, ea, A, T, seed, gamma)
+    _one_launch(fp, eb, B, T, seed, gamma, chunks)
+    for k in ("obs_copy", "actions", "log_prob", "value", "episode_starts", "rewards", "last_obs",
+              "last_start", "ep_ret", "ep_len"):
+        a, b = A[k].cpu().numpy(), B[k].cpu().numpy()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), \
+            f"{k}: {np.sum(a.view(np.uint32) != b.view(np.uint32))} words differ"
+    sa, sb = ea.get_state(), eb.get_state()
+    for k, v in sa.items():
+        assert np.array_equal(np.asarray(v).view(np.uint32), np.asarray(sb[k]).view(np.uint32)), k
+    ta, tb = A["stats"].sum(0).cpu().numpy(), B["stats"].sum(0).cpu().numpy()
+    np.testing.assert_allclose(tb, ta, rtol=1e-6)
+    # the case exercised what it claims: resets, and (short limits) time-limit bootstraps
+    starts = B["episode_starts"].cpu().numpy()
+    last = B["last_start"].cpu().numpy()
+    done = np.concatenate([starts[1:], last[None]], 0)  # done[t] = env finished at step t
+    assert done.sum() > 0 and tb[2] == done.sum()
+    if max_steps <= T:
+        length = np.zeros(n)
+        truncs = 0
+        for t in range(T):
+            length += 1
+            truncs += int(np.sum((done[t] == 1) & (length == max_steps)))
+            length[done[t] == 1] = 0
+        assert truncs > 0
+
+
+def test_rollout_rejects_bad_arguments():
+    from uav_reinforcement_learning_control_amd import _native as N
+    from uav_reinforcement_learning_control_amd.ppo.fused import FusedPolicy, rollout_supported
+    fp = FusedPolicy(_policy())
+    fp.pack()
+    n = 64
+    env = _env(n, "hover", "RelPosActWrapper", 512)
+    assert not rollout_supported(env)
+    b = _bufs(4, n)
+    with pytest.raises(N.QuadError):
+        fp.rollout(env, t0=0, steps=4, seed=1, gamma=0.99, **b)  # 7-D obs: rejected by the ABI
+    env2 = _env(n, "hover", None, 512)
+    assert rollout_supported(env2)
+    with pytest.raises(N.QuadError):
+        fp.rollout(env2, t0=0, steps=0, seed=1, gamma=0.99, **b)
+    with pytest.raises(ValueError):
+        fp.rollout(env2, t0=0, steps=1, seed=1, gamma=0.99, **dict(b, ep_len=torch.zeros(n + 1, device="cuda")))
+
+
+def test_ppo_collect_one_launch_and_two_launch():
+    """PPO.collect_rollouts through quad_rollout (default) and through the graph-captured
+    two-launch path: both fill the buffers, finish episodes, and feed the update. (Their rows are
+    not compared: the two-launch path's graph capture steps the env once before its first rollout;
+    the bit-level equivalence is test_one_launch_rollout_is_bit_identical.)"""
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
+    n, T = 2048, 32
+    outs = []
+    for one in (False, True):
+        env = _env(n, "hover", None, 512, seed=11)
+        cfg = PPOConfig(n_steps=T, n_epochs=1, n_minibatches=4, fused_rollout=one)
+        ppo = PPO(env, cfg, seed=3)
+        assert ppo._one_launch == one
+        rs = ppo.collect_rollouts()
+        outs.append((rs, {k: getattr(ppo, k).clone() for k in ("buf_rew", "buf_val", "buf_logp", "buf_adv",
+                                                               "buf_ret", "buf_start")}))
+        assert rs.env_steps == n * T and torch.isfinite(ppo.buf_adv).all()
+        ppo.train(max_minibatches=2)  # the update runs on the one-launch buffers
+        rs2 = ppo.collect_rollouts()
+        assert rs2.env_steps == n * T
+    (ra, _), (rb, _) = outs
+    assert ra.episodes > 0 and rb.episodes > 0
+    assert abs(ra.mean_length - rb.mean_length) < 0.5 * max(ra.mean_length, rb.mean_length)

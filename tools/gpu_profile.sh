@@ -15,10 +15,14 @@ run() {
   echo "=== $name rc=$rc"; tail -n 3 "$O/$name.log"
   if [ $rc -ne 0 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
 }
-B="python bench.py --no-cpu-baseline --steps 400 --warmup 100"
+# kernel trace of the bench (no end-to-end PPO iteration: its ~250k torch launches would make a
+# >64 MiB trace); PMC passes on a minimal driver (tools/step_once.py: eager quad_step launches)
+B="python bench.py --no-cpu-baseline --e2e-iters 0 --steps 400 --warmup 100"
 run trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- $B
-run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o bench -- $B
-run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o bench -- $B
+for N in 65536 1048576; do
+  run pmc_fetch_$N 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch/$N -o step -- python tools/step_once.py $N 100
+  run pmc_write_$N 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write/$N -o step -- python tools/step_once.py $N 100
+done
 run pmc_cal_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_cal_fetch -o cal -- tools/pmc/_build/pmc_calib
 run pmc_cal_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_cal_write -o cal -- tools/pmc/_build/pmc_calib
 echo "=== done"

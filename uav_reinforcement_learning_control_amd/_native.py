@@ -15,7 +15,7 @@ CSRC = os.path.join(_PKG, "csrc")
 QUAD_OK, QUAD_EINVAL, QUAD_EHIP, QUAD_ENOMEM, QUAD_EMODEL = 0, -1, -2, -3, -4
 ENV_HOVER, ENV_TRAJ, ENV_BRAX_HOVER, ENV_BRAX_TRAJ = 0, 1, 2, 3
 WRAP_NONE, WRAP_CTBR, WRAP_RELPOS = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class QuadCfg(C.Structure):
@@ -94,8 +94,16 @@ class QuadPolicyAct(C.Structure):
 EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_create",
            "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
            "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
-           "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post",
+           "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
            "quad_waypoints_begin", "quad_waypoints_update")
+
+
+class QuadRollout(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("obs_copy", "actions", "log_prob", "value", "episode_starts",
+                                          "rewards", "last_obs", "last_start", "ep_ret", "ep_len",
+                                          "stats")] + \
+               [("rows", C.c_int32), ("t0", C.c_int32), ("steps", C.c_int32), ("deterministic", C.c_int32),
+                ("seed", C.c_uint64), ("gamma", C.c_float)]
 
 
 class QuadError(RuntimeError):
@@ -129,12 +137,13 @@ def _declare(L):
     L.quad_policy_pack.argtypes = [C.POINTER(QuadPolicyParams), vp, vp]
     L.quad_policy_act.argtypes = [vp, C.POINTER(QuadPolicyAct), i32, vp]
     L.quad_rollout_post.argtypes = [vp, C.POINTER(QuadRolloutPost), vp, i32, vp]
+    L.quad_rollout.argtypes = [vp, vp, C.POINTER(QuadRollout), vp]
     L.quad_waypoints_begin.argtypes = [vp, C.POINTER(QuadWaypoints), C.POINTER(QuadWaypointState), vp, vp]
     L.quad_waypoints_update.argtypes = [vp, C.POINTER(QuadWaypoints), C.POINTER(QuadWaypointState),
                                         vp, vp, vp, vp, vp]
     for n in ("quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
-              "quad_policy_pack", "quad_policy_act", "quad_rollout_post",
+              "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
               "quad_waypoints_begin", "quad_waypoints_update"):
         getattr(L, n).restype = C.c_int
 

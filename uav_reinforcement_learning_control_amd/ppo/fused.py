@@ -112,3 +112,35 @@ class FusedPolicy:
         _need(cursor, (4,), torch.int32, self.device, "cursor")
         N.check(N.lib().quad_rollout_post(_p(self.packed), C.byref(epilogue), _p(cursor), epilogue._n,
                                           self._stream()), "quad_rollout_post")
+
+    def rollout(self, env, *, obs_copy, actions, log_prob, value, episode_starts, rewards, last_obs,
+                last_start, ep_ret, ep_len, stats, t0: int, steps: int, seed: int, gamma: float,
+                deterministic: bool = False) -> None:
+        """quad_rollout: `steps` whole rollout steps (policy + env step + bootstrap + statistics)
+        of `env` (a QuadVecEnv: hover/trajectory, no wrapper or RateControlWrapper, auto-reset) in
+        one launch; step t = t0 + s writes row t % rows of the [rows, N, ...] buffers."""
+        n, dev, f32 = env.num_envs, self.device, torch.float32
+        rows = rewards.shape[0]
+        for t, shp, name in ((obs_copy, (rows, n, 12), "obs_copy"), (actions, (rows, n, 4), "actions"),
+                             (log_prob, (rows, n), "log_prob"), (value, (rows, n), "value"),
+                             (episode_starts, (rows, n), "episode_starts"), (rewards, (rows, n), "rewards"),
+                             (last_obs, (n, 12), "last_obs"), (last_start, (n,), "last_start"),
+                             (ep_ret, (n,), "ep_ret"), (ep_len, (n,), "ep_len")):
+            _need(t, shp, f32, dev, name)
+        _need(stats, (N.POLICY_STAT_SLOTS, 3), torch.float64, dev, "stats")
+        r = N.QuadRollout(obs_copy=obs_copy.data_ptr(), actions=actions.data_ptr(),
+                          log_prob=log_prob.data_ptr(), value=value.data_ptr(),
+                          episode_starts=episode_starts.data_ptr(), rewards=rewards.data_ptr(),
+                          last_obs=last_obs.data_ptr(), last_start=last_start.data_ptr(),
+                          ep_ret=ep_ret.data_ptr(), ep_len=ep_len.data_ptr(), stats=stats.data_ptr(),
+                          rows=int(rows), t0=int(t0), steps=int(steps),
+                          deterministic=int(bool(deterministic)), seed=int(seed) & (2**64 - 1),
+                          gamma=float(gamma))
+        N.check(N.lib().quad_rollout(env._h, _p(self.packed), C.byref(r), self._stream()), "quad_rollout")
+
+
+def rollout_supported(env) -> bool:
+    """quad_rollout drives hover / trajectory envs (12-D obs) with SB3 auto-reset."""
+    cfg = getattr(env, "cfg", None)
+    return (cfg is not None and getattr(env, "_h", None) is not None and cfg.auto_reset == 1
+            and cfg.env_kind in (N.ENV_HOVER, N.ENV_TRAJ) and cfg.wrapper in (N.WRAP_NONE, N.WRAP_CTBR))

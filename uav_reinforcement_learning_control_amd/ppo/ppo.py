@@ -29,7 +29,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from .. import _native as N
-from .fused import FusedPolicy
+from .fused import FusedPolicy, rollout_supported
 from .gae import gae
 from .policy import ActorCritic
 
@@ -51,6 +51,8 @@ class PPOConfig:
     net_arch: tuple = (128, 128)
     adam_eps: float = 1e-5
     fused_policy: bool = True             # rollout policy on the MFMA kernels (ppo/fused.py)
+    fused_rollout: bool = True            # whole rollout as quad_rollout launches (needs fused_policy)
+    rollout_chunk: int = 1024             # steps per quad_rollout launch
 
 
 def ppo_loss(policy: ActorCritic, obs, act, logp_old, adv, ret, cfg: PPOConfig):
@@ -146,6 +148,9 @@ class PPO:
             self._epi = self._fp.make_epilogue(env.reward, env.terminated, env.truncated,
                                                env.terminal_obs, self.buf_rew, self.last_start,
                                                self.ep_ret, self.ep_len, self._slots, T, self.cfg.gamma)
+        # one launch per chunk of steps: policy + env + bootstrap + statistics (csrc/rollout.hip)
+        self._one_launch = (self._fp is not None and self.cfg.fused_rollout and rollout_supported(env))
+        self._t_host = 0  # running step counter of the one-launch path (keys the action noise)
         self._noise_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5851F42D4C957F2D) & (2**64 - 1)
 
     # ------------------------------------------------------------------------------------
@@ -221,8 +226,10 @@ class PPO:
             self.last_obs.copy_(env.reset())
             self.last_start.fill_(1.0)
             self._started = True
-            if use_graph:
+            if use_graph and not self._one_launch:
                 self._capture()
+        if self._one_launch:
+            return self._collect_one_launch()
         t0 = time.perf_counter()
         self._t.zero_()
         self._done_stats.zero_()
@@ -237,6 +244,36 @@ class PPO:
         if self._fp is not None:
             self._fp.post(self._epi, self._cursor)   # finish the last step
             self._done_stats.copy_(self._slots.sum(0))
+        last_v = pol.value(self.last_obs)
+        gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
+            cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
+        torch.cuda.synchronize(self.device)
+        steps = cfg.n_steps * env.num_envs
+        self.num_timesteps += steps * self.world
+        ret_sum, len_sum, c = self._done_stats.tolist()
+        return RolloutStats(episodes=int(c), mean_return=ret_sum / c if c else float("nan"),
+                            mean_length=len_sum / c if c else float("nan"),
+                            env_steps=steps, seconds=time.perf_counter() - t0)
+
+    @torch.no_grad()
+    def _collect_one_launch(self) -> RolloutStats:
+        """collect_rollouts as quad_rollout launches (rollout_chunk steps each): same buffers, same
+        semantics as the two-launch path, no per-step launches or HBM round trips of env state."""
+        env, cfg, pol = self.env, self.cfg, self.policy
+        t0 = time.perf_counter()
+        self._slots.zero_()
+        chunk = max(1, min(int(cfg.rollout_chunk), cfg.n_steps))
+        s = 0
+        while s < cfg.n_steps:
+            k = min(chunk, cfg.n_steps - s)
+            self._fp.rollout(env, obs_copy=self.buf_obs, actions=self.buf_act, log_prob=self.buf_logp,
+                             value=self.buf_val, episode_starts=self.buf_start, rewards=self.buf_rew,
+                             last_obs=self.last_obs, last_start=self.last_start, ep_ret=self.ep_ret,
+                             ep_len=self.ep_len, stats=self._slots, t0=self._t_host + s, steps=k,
+                             seed=self._noise_seed, gamma=cfg.gamma)
+            s += k
+        self._t_host += cfg.n_steps
+        self._done_stats.copy_(self._slots.sum(0))
         last_v = pol.value(self.last_obs)
         gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
             cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
