@@ -8,7 +8,17 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-FUSED = pytest.mark.parametrize("fused", [True, False], ids=["mfma", "torch"])
+# "one": quad_rollout (one launch per rollout chunk, the default); "mfma": policy kernel + env
+# step per step (graph-replayed); "torch": the torch policy + env step
+FUSED = pytest.mark.parametrize("fused", ["one", "mfma", "torch"])
+
+
+def _path(fused):
+    return dict(fused_policy=fused != "torch", fused_rollout=fused == "one")
+
+
+def _t_of(m, fused):
+    return {"one": lambda: m._t_host, "mfma": lambda: m._cursor[0].item(), "torch": lambda: m._t.item()}[fused]()
 
 
 def _ppo(n, T, **kw):
@@ -20,7 +30,7 @@ def _ppo(n, T, **kw):
 
 @FUSED
 def test_graph_rollout_buffers_are_consistent(fused):
-    m = _ppo(2048, 24, n_epochs=1, n_minibatches=4, fused_policy=fused)
+    m = _ppo(2048, 24, n_epochs=1, n_minibatches=4, **_path(fused))
     rs = m.collect_rollouts(use_graph=True)
     rs = m.collect_rollouts(use_graph=True)
     with torch.no_grad():
@@ -34,25 +44,28 @@ def test_graph_rollout_buffers_are_consistent(fused):
     # an episode start follows every done: starts are 0/1 and many episodes ended (random policy)
     st = m.buf_start.cpu().numpy()
     assert set(np.unique(st)) <= {0.0, 1.0} and rs.episodes > 0
-    assert (m._cursor[0].item() == 48 and m._cursor[1].item() == 0) if fused else (m._t.item() == 24)
+    assert _t_of(m, fused) == (24 if fused == "torch" else 48)
+    if fused == "mfma":
+        assert m._cursor[1].item() == 0
     # the obs rows chain: obs[t+1] of an env that did not finish is the env's next obs
     assert torch.isfinite(m.buf_obs).all() and torch.all(m.buf_obs.abs() <= 1.0 + 1e-6)
 
 
 @FUSED
 def test_eager_and_graph_rollouts_agree_on_semantics(fused):
-    m = _ppo(1024, 8, n_epochs=1, n_minibatches=2, fused_policy=fused)
+    m = _ppo(1024, 8, n_epochs=1, n_minibatches=2, **_path(fused))
     m.collect_rollouts(use_graph=False)
-    assert ((m._cursor[0].item() == 8) if fused else (m._t.item() == 8)) and torch.isfinite(m.buf_ret).all()
+    assert _t_of(m, fused) == 8 and torch.isfinite(m.buf_ret).all()
 
 
-def test_fused_rollout_matches_replayed_env():
+@pytest.mark.parametrize("one", [True, False], ids=["one", "mfma"])
+def test_fused_rollout_matches_replayed_env(one):
     """Replay the fused rollout's unclipped actions through a fresh env with the same seed: the
     rewards (after the TimeLimit bootstrap is removed), episode starts and obs rows must agree
     bit for bit -- the epilogue only moves env outputs into the buffers."""
     from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
     n, T = 512, 16
-    m = _ppo(n, T, n_epochs=1, n_minibatches=2, fused_policy=True)
+    m = _ppo(n, T, n_epochs=1, n_minibatches=2, fused_policy=True, fused_rollout=one)
     m.collect_rollouts(use_graph=False)
     env2 = QuadVecEnv(n, wrapper="RateControlWrapper", device="cuda:0", seed=3)
     obs = env2.reset().clone()
@@ -68,7 +81,7 @@ def test_fused_rollout_matches_replayed_env():
 
 @FUSED
 def test_short_training_makes_progress(fused):
-    m = _ppo(4096, 64, n_epochs=4, n_minibatches=8, learning_rate=3e-4, fused_policy=fused)
+    m = _ppo(4096, 64, n_epochs=4, n_minibatches=8, learning_rate=3e-4, **_path(fused))
     lens = []
     for it in range(12):
         rs = m.collect_rollouts()
