@@ -80,7 +80,10 @@ def _one_launch(fp, env, b, T, seed, gamma, chunks):
     ("trajectory", "RateControlWrapper", 11, 777, (5, 5, 10)),
     ("hover", None, 512, 65536, (20,)),
 ])
-def test_one_launch_rollout_is_bit_identical(kind, wrapper, max_steps, n, chunks):
+@pytest.mark.parametrize("nt", ["2", "1"])
+def test_one_launch_rollout_is_bit_identical(kind, wrapper, max_steps, n, chunks, nt, monkeypatch):
+    # nt: tiles per wave of k_rollout (2 = product default; 1 = the A/B form, read per launch)
+    monkeypatch.setenv("QUADENV_ROLLOUT_NT", nt)
     from uav_reinforcement_learning_control_amd.ppo.fused import FusedPolicy
     T, seed, gamma = sum(chunks), 0x1234_5678_9ABC, 0.97
     fp = FusedPolicy(_policy())

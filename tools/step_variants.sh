@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../uav_reinforcement_learning_control_amd/csrc"
 mkdir -p ../../tools/_build
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-function -ffp-contract=fast-honor-pragmas"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-function -ffp-contract=on"
 for v in PHYS2 NOPHYS NOOBS NORESET; do
   /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DQD_ABL_$v -o ../../tools/_build/abl_$v.so quadenv.hip policy.hip &
 done

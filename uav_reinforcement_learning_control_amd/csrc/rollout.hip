@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/quadenv.h"
 #include "env_tiles.h"
@@ -35,38 +36,48 @@ namespace quadenv {
 
 namespace {
 
-constexpr int RBLOCK = 256;  // 4 waves = 4 x 64 envs; one block per CU (the LDS holds the nets)
+constexpr int RBLOCK = 256;  // envs per block; one block per CU (the LDS holds the nets)
+constexpr int ROLLOUT_NT_DEFAULT = 2;
 
-// X^T fragments of the wave's two tiles from the per-thread observation rows (see top).
-__device__ __forceinline__ void tile_fragments(const float ob[12], float xb[2][6]) {
+// X^T fragments of the wave's tile(s) from the per-thread observation rows (see top).
+template <int NT>
+__device__ __forceinline__ void fragments(const float ob[12], float (&xb)[NT][6]) {
   const bool h = (threadIdx.x & 32) != 0;
 #pragma unroll
   for (int s = 0; s < 6; s++) {
     const float lo = ob[2 * s], hi = ob[2 * s + 1];
-    const float got = __shfl_xor(h ? lo : hi, 32);
-    xb[0][s] = h ? got : lo;
-    xb[1][s] = h ? hi : got;
+    if constexpr (NT == 2) {  // lane l's env is tile (l >> 5)'s env l & 31
+      const float got = __shfl_xor(h ? lo : hi, 32);
+      xb[0][s] = h ? got : lo;
+      xb[NT - 1][s] = h ? hi : got;
+    } else {  // both lane halves carry env l & 31
+      xb[0][s] = h ? hi : lo;
+    }
   }
 }
 
 // The reset draws of the wave's resetting envs, compacted across the wave as in k_step
 // (quadenv.hip reset_words_wave): one Philox pass of (env, block) items for up to 16 resetting
-// lanes. The words travel by lane shuffles instead of LDS (the nets fill it). Identical words.
+// envs. The words travel by lane shuffles instead of LDS (the nets fill it). Identical words.
+// `publish`: this lane lists its env (one lane per env); `apply`: this lane takes the words of the
+// env listed under key `key` (KEY_MASK = 31 when lanes l and l + 32 carry the same env).
+template <int KEY_MASK>
 __device__ __forceinline__ void reset_words_shfl(const KParams& p, uint32_t (&renv)[64], uint32_t (&rep)[64],
-                                                 uint32_t i, uint32_t ep, bool rs, uint32_t r16[16]) {
-  const uint64_t m = __ballot(rs);
+                                                 uint32_t i, uint32_t ep, bool publish, bool apply,
+                                                 uint32_t r16[16]) {
+  const uint64_t m = __ballot(publish);
   if (m == 0) return;
   const int lane = __lane_id();
   const int nres = __popcll(m);
-  const int rank = __popcll(m & __lanemask_lt());
-  if (rs) { renv[rank] = i; rep[rank] = ep; }
+  const int rank = __popcll(m & ((1ull << (lane & KEY_MASK)) - 1ull));
+  if (publish) { renv[rank] = i; rep[rank] = ep; }
   __builtin_amdgcn_wave_barrier();
   const int passes = (nres * 4 + 63) >> 6;
   for (int t = 0; t < passes; t++) {
     const int item = t * 64 + lane, rr = item >> 2;
     uint32_t c[4] = {0u, 0u, 0u, 0u};
     if (rr < nres) reset_block(p.seed, p.gid_base + uint64_t(renv[rr]), rep[rr], uint32_t(item & 3), c);
-    const bool mine = rs && (rank >> 4) == t;
+    const bool mine = apply && (rank >> 4) == t;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const int src = (rank * 4 + b) & 63;
@@ -87,16 +98,22 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, size_t row, 
   b4[2] = make_float4(v[8], v[9], v[10], v[11]);
 }
 
-template <int KIND, bool CTBR>
-__global__ __launch_bounds__(RBLOCK) void k_rollout(const KConsts<float>* __restrict__ kc, KParams p,
-                                                    const float* __restrict__ packed, RollArgs a) {
+// NT = 2: 4 waves (one per SIMD), wave w owns envs 64w .. 64w + 63 = its two MFMA tiles.
+// NT = 1: 8 waves (two per SIMD), wave w owns the 32 envs 32w .. 32w + 31 = one tile; lanes l and
+// l + 32 both carry env l & 31 (the same state, the same action, bit for bit), so the tile's X^T
+// fragment needs no exchange, and one wave's env step (VALU) can run under the other wave's MFMA.
+template <int KIND, bool CTBR, int NT>
+__global__ __launch_bounds__(512 / NT) void k_rollout(const KConsts<float>* __restrict__ kc, KParams p,
+                                                            const float* __restrict__ packed, RollArgs a) {
+  constexpr int BLK = 512 / NT, WAVES = BLK / 64;
   p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
   extern __shared__ float lds[];
-  __shared__ uint32_t renv[RBLOCK / 64][64], rep[RBLOCK / 64][64];
+  __shared__ uint32_t renv[WAVES][64], rep[WAVES][64];
   const int w = threadIdx.x >> 6;
   const bool h = (threadIdx.x & 32) != 0;
-  const int i_raw = blockIdx.x * RBLOCK + threadIdx.x;
+  const int i_raw = blockIdx.x * RBLOCK + (NT == 2 ? int(threadIdx.x) : w * 32 + int(threadIdx.x & 31));
   const bool ok = i_raw < p.n;
+  const bool owner = ok && (NT == 2 || !h);  // the lane that stores this env's outputs
   // lanes past the last env shadow it (in-range loads, MFMA columns of their own) and store nothing
   const int i = ok ? i_raw : p.n - 1;
   const size_t n = size_t(p.n);
@@ -116,7 +133,7 @@ __global__ __launch_bounds__(RBLOCK) void k_rollout(const KConsts<float>* __rest
     ob[8] = x2.x; ob[9] = x2.y; ob[10] = x2.z; ob[11] = x2.w;
   }
   float ls = a.last_start[i], ret = a.ep_ret[i], len = a.ep_len[i];
-  stage_lds<RBLOCK>(lds, packed);
+  stage_lds<BLK>(lds, packed);
   const float* log_std = packed + LDS_F;
   float lstd[ACT], sd[ACT];
 #pragma unroll
@@ -127,46 +144,67 @@ __global__ __launch_bounds__(RBLOCK) void k_rollout(const KConsts<float>* __rest
     const uint32_t t = a.t0 + uint32_t(s);
     const size_t row = size_t(t % a.rows) * n + size_t(i);
     // ---- policy: both nets on the wave's two tiles, then this lane's env
-    float xb[2][6], mean[2][ACT], val[2][1];
-    tile_fragments(ob, xb);
-    net_forward<ACT, 2>(lds, xb, mean);
-    net_forward<1, 2>(lds + ACTOR_F, xb, val);
+    float xb[NT][6], mean[NT][ACT], val[NT][1];
+    fragments<NT>(ob, xb);
+    // QD_ROLL_*: cost-ablation builds of tools/rollout_variants.py only (never defined in the product)
+#if defined(QD_ROLL_NOMLP)
+#pragma unroll
+    for (int j = 0; j < NT; j++) {
+      val[j][0] = xb[j][0];
+#pragma unroll
+      for (int k = 0; k < ACT; k++) mean[j][k] = xb[j][k];
+    }
+#else
+    net_forward<ACT, NT>(lds, xb, mean);
+#if defined(QD_ROLL_NOCRITIC)
+#pragma unroll
+    for (int j = 0; j < NT; j++) val[j][0] = mean[j][0];
+#else
+    net_forward<1, NT>(lds + ACTOR_F, xb, val);
+#endif
+#endif
     float z[ACT] = {0.f, 0.f, 0.f, 0.f};
     if (!a.deterministic) gauss4(a.seed, p.gid_base + uint64_t(i), t, z);
     float act[ACT], ac[ACT], lp = 0.f;
 #pragma unroll
     for (int k = 0; k < ACT; k++) {
-      const float mk = h ? mean[1][k] : mean[0][k];
+      const float mk = (NT == 2 && h) ? mean[NT - 1][k] : mean[0][k];
       act[k] = mk + sd[k] * z[k];
       const float zz = (act[k] - mk) / sd[k];  // as PPO.train recomputes it (policy.log_prob)
       lp += -0.5f * zz * zz - lstd[k] - 0.91893853320467274f;  // 0.5 log(2 pi)
       ac[k] = fminf(fmaxf(act[k], -1.f), 1.f);
     }
-    if (ok) {
+    if (owner) {
       store_row(a.obs_copy, row, ob);
       reinterpret_cast<float4*>(a.actions)[row] = make_float4(act[0], act[1], act[2], act[3]);
       a.log_prob[row] = lp;
-      a.value[row] = h ? val[1][0] : val[0][0];
+      a.value[row] = (NT == 2 && h) ? val[NT - 1][0] : val[0][0];
       a.starts[row] = ls;
     }
     // ---- env step (HoverEnv.step / TrajectoryFollowEnv.step, RateControlWrapper.action)
     StepRes r;
+#if defined(QD_ROLL_NOENV)
+#pragma unroll
+    for (int j = 0; j < 12; j++) r.obs[j] = fminf(fmaxf(ob[j] + 1e-3f * ac[j & 3], -1.f), 1.f);
+    r.reward = ac[0]; r.term = false; r.trunc = false;
+#else
     env_step<float, CTBR>(*p.kc, e, ac, r);
+#endif
     const bool done = r.term || r.trunc;
     // ---- TimeLimit bootstrap: r += gamma V(terminal_obs) (critic only if the wave holds one)
     const bool timeout = ok && r.trunc && !r.term;
     float tv = 0.f;
     if (__any(timeout)) {
-      float xt[2][6], vt[2][1];
-      tile_fragments(r.obs, xt);
-      net_forward<1, 2>(lds + ACTOR_F, xt, vt);
-      tv = h ? vt[1][0] : vt[0][0];
+      float xt[NT][6], vt[NT][1];
+      fragments<NT>(r.obs, xt);
+      net_forward<1, NT>(lds + ACTOR_F, xt, vt);
+      tv = (NT == 2 && h) ? vt[NT - 1][0] : vt[0][0];
     }
     // ---- reward row, Monitor statistics, episode_starts of the next step
     const float rret = ret + r.reward, rlen = len + 1.f;
-    if (ok) {
+    if (owner) {
       a.rewards[row] = timeout ? r.reward + a.gamma * tv : r.reward;
-      if (done) { st[0] += double(rret); st[1] += double(rlen); st[2] += 1.0; }
+      if (done) { st[0] += double(rret); st[1] += double(rlen); st[2] += 1.0; }  // owner lanes only
     }
     ret = done ? 0.f : rret;
     len = done ? 0.f : rlen;
@@ -176,7 +214,7 @@ __global__ __launch_bounds__(RBLOCK) void k_rollout(const KConsts<float>* __rest
     // ---- SB3 auto-reset: the next step starts from the reset observation
     const bool rs = ok && done;
     uint32_t r16[16];
-    reset_words_shfl(p, renv[w], rep[w], uint32_t(i), ep, rs, r16);
+    reset_words_shfl<NT == 2 ? 63 : 31>(p, renv[w], rep[w], uint32_t(i), ep, owner && done, rs, r16);
     if (rs) {
       float init12[12], tgt[3], s12[12];
       reset_affine(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, r16, init12, tgt);
@@ -186,7 +224,7 @@ __global__ __launch_bounds__(RBLOCK) void k_rollout(const KConsts<float>* __rest
   }
 
   // ---- carry the rollout to the next call
-  if (ok) {
+  if (owner) {
     store_env(p, i, e, CTBR);
     S.stu(F_EP, vo, ep);
     store_row(a.last_obs, size_t(i), ob);
@@ -195,7 +233,7 @@ __global__ __launch_bounds__(RBLOCK) void k_rollout(const KConsts<float>* __rest
     a.ep_len[i] = len;
   }
   // Monitor statistics: block sum into this block's slot (uncontended double atomics)
-  __shared__ double red[3][RBLOCK / 64];
+  __shared__ double red[3][WAVES];
 #pragma unroll
   for (int j = 0; j < 3; j++) {
     double v = st[j];
@@ -205,12 +243,12 @@ __global__ __launch_bounds__(RBLOCK) void k_rollout(const KConsts<float>* __rest
   __syncthreads();
   if (threadIdx.x < 3) {
     double s = 0.0;
-    for (int k = 0; k < RBLOCK / 64; k++) s += red[threadIdx.x][k];
+    for (int k = 0; k < WAVES; k++) s += red[threadIdx.x][k];
     if (s != 0.0) atomicAdd(&a.stats[(blockIdx.x % QUAD_POLICY_STAT_SLOTS) * 3 + threadIdx.x], s);
   }
 }
 
-template <int KIND, bool CTBR>
+template <int KIND, bool CTBR, int NT>
 hipError_t launch(const KConsts<float>* kc, const KParams& kp, const float* packed, const RollArgs& a,
                   hipStream_t s) {
   static bool opted[64] = {};
@@ -218,23 +256,34 @@ hipError_t launch(const KConsts<float>* kc, const KParams& kp, const float* pack
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   const int bytes = LDS_F * int(sizeof(float));
   if (!opted[dev]) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rollout<KIND, CTBR>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rollout<KIND, CTBR, NT>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
     opted[dev] = true;
   }
-  hipLaunchKernelGGL((k_rollout<KIND, CTBR>), dim3((kp.n + RBLOCK - 1) / RBLOCK), dim3(RBLOCK), bytes, s, kc,
-                     kp, packed, a);
+  hipLaunchKernelGGL((k_rollout<KIND, CTBR, NT>), dim3((kp.n + RBLOCK - 1) / RBLOCK), dim3(512 / NT), bytes,
+                     s, kc, kp, packed, a);
   return hipGetLastError();
 }
 
 }  // namespace
 
+template <int NT>
+hipError_t launch_nt(const KConsts<float>* kc, const KParams& kp, int env_kind, bool ctbr, const float* packed,
+                     const RollArgs& a, hipStream_t s) {
+  if (env_kind == QUAD_ENV_TRAJ)
+    return ctbr ? launch<QUAD_ENV_TRAJ, true, NT>(kc, kp, packed, a, s)
+                : launch<QUAD_ENV_TRAJ, false, NT>(kc, kp, packed, a, s);
+  return ctbr ? launch<QUAD_ENV_HOVER, true, NT>(kc, kp, packed, a, s)
+              : launch<QUAD_ENV_HOVER, false, NT>(kc, kp, packed, a, s);
+}
+
 hipError_t launch_rollout(const KConsts<float>* kc, const KParams& kp, int env_kind, bool ctbr,
                           const float* packed, const RollArgs& a, hipStream_t s) {
-  if (env_kind == QUAD_ENV_TRAJ)
-    return ctbr ? launch<QUAD_ENV_TRAJ, true>(kc, kp, packed, a, s) : launch<QUAD_ENV_TRAJ, false>(kc, kp, packed, a, s);
-  return ctbr ? launch<QUAD_ENV_HOVER, true>(kc, kp, packed, a, s) : launch<QUAD_ENV_HOVER, false>(kc, kp, packed, a, s);
+  const char* v = std::getenv("QUADENV_ROLLOUT_NT");  // A/B override: 1 or 2 tiles per wave
+  const int nt = v && std::atoi(v) == 1 ? 1 : (v && std::atoi(v) == 2 ? 2 : ROLLOUT_NT_DEFAULT);
+  return nt == 1 ? launch_nt<1>(kc, kp, env_kind, ctbr, packed, a, s)
+                 : launch_nt<2>(kc, kp, env_kind, ctbr, packed, a, s);
 }
 
 }  // namespace quadenv
