@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define QUADENV_ABI_VERSION 3
+#define QUADENV_ABI_VERSION 4
 
 enum { QUAD_OK = 0, QUAD_EINVAL = -1, QUAD_EHIP = -2, QUAD_ENOMEM = -3, QUAD_EMODEL = -4 };
 /* QUAD_ENV_BRAX_HOVER / QUAD_ENV_BRAX_TRAJ: the brax Env API siblings of the same path
@@ -319,6 +319,42 @@ typedef struct QuadRollout {
   float gamma;
 } QuadRollout;
 int quad_rollout(QuadHandle* h, const float* packed, const QuadRollout* r, void* stream);
+
+/* ---- PPO minibatch gradient on MFMA (row P): the gradient of SB3 PPO.train's minibatch loss
+ * (stable_baselines3 ppo.py, as train.py:50-68 configures it; ppo/ppo.py ppo_loss restates it)
+ *   loss = -mean(min(A r, A clip(r, 1 - clip_range, 1 + clip_range)))
+ *          + ent_coef * (-entropy) + vf_coef * mean((returns - V)^2),
+ *   r = exp(log_prob(actions) - old_log_prob), A = (adv - mean(adv)) / (std(adv) + 1e-8) over the
+ *   minibatch (unbiased std; skipped when normalize_advantage == 0 or batch == 1),
+ * with respect to every policy parameter, for the ActorCritic of QuadPolicyParams. Rows of the
+ * flattened rollout buffer are gathered through `index` (a slice of the epoch's permutation), so
+ * no minibatch copy is made. Ties of the min and the clip bounds follow torch's autograd
+ * (torch.min splits a tie's gradient in half; clamp passes it on the closed interval). Gradients
+ * are OVERWRITTEN (not accumulated) into `grads` (same shapes as the parameters); nothing in the
+ * launch sequence synchronizes the host, so it is graph-capturable. */
+typedef struct QuadPolicyGrads {
+  float *pi_w0, *pi_b0, *pi_w1, *pi_b1, *act_w, *act_b;
+  float *vf_w0, *vf_b0, *vf_w1, *vf_b1, *val_w, *val_b;
+  float* log_std;
+} QuadPolicyGrads;
+
+typedef struct QuadPPOBatch {
+  const float* obs;         /* [M,12] rollout buffer rows (16-byte aligned) */
+  const float* actions;     /* [M,4] unclipped actions (16-byte aligned) */
+  const float* log_prob;    /* [M] old log-probabilities */
+  const float* advantages;  /* [M] */
+  const float* returns;     /* [M] */
+  const int64_t* index;     /* [batch] rows of this minibatch, each in [0, M) */
+  int32_t batch;            /* >= 1 */
+  int32_t normalize_advantage;
+  float clip_range, ent_coef, vf_coef;
+  float* stats;             /* [4] out, or NULL: pg_loss, vf_loss, entropy, clip_fraction */
+} QuadPPOBatch;
+
+/* Device workspace (bytes) quad_ppo_grad needs for a minibatch of `batch` rows. */
+int64_t quad_ppo_workspace_bytes(int32_t batch);
+int quad_ppo_grad(const QuadPolicyParams* params, const QuadPPOBatch* b, const QuadPolicyGrads* grads,
+                  void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -16,7 +16,7 @@ HEADER = os.path.join(REPO, "include", "quadenv.h")
 
 def _declared():
     src = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|int32_t|const char\*)\s+(quad_\w+)\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|int32_t|int64_t|const char\*)\s+(quad_\w+)\(", src, re.M)))
 
 
 def test_library_loads_and_version():
@@ -48,6 +48,8 @@ int main(void) {{
   printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(QuadPolicyParams), sizeof(QuadPolicyAct),
          offsetof(QuadPolicyAct, rows), offsetof(QuadPolicyAct, env_id_base),
          sizeof(QuadRolloutPost), offsetof(QuadRolloutPost, rows), offsetof(QuadRolloutPost, gamma));
+  printf("%zu %zu %zu %zu %zu\\n", sizeof(QuadPolicyGrads), sizeof(QuadPPOBatch), offsetof(QuadPPOBatch, batch),
+         offsetof(QuadPPOBatch, vf_coef), offsetof(QuadPPOBatch, stats));
   return 0;
 }}''')
     exe = tmp_path / "layout"
@@ -57,7 +59,9 @@ int main(void) {{
             C.sizeof(N.QuadStepOut), N.QuadStepOut.state12.offset, C.sizeof(N.QuadStateSoA),
             C.sizeof(N.QuadPolicyParams), C.sizeof(N.QuadPolicyAct), N.QuadPolicyAct.rows.offset,
             N.QuadPolicyAct.env_id_base.offset, C.sizeof(N.QuadRolloutPost),
-            N.QuadRolloutPost.rows.offset, N.QuadRolloutPost.gamma.offset]
+            N.QuadRolloutPost.rows.offset, N.QuadRolloutPost.gamma.offset,
+            C.sizeof(N.QuadPolicyGrads), C.sizeof(N.QuadPPOBatch), N.QuadPPOBatch.batch.offset,
+            N.QuadPPOBatch.vf_coef.offset, N.QuadPPOBatch.stats.offset]
     assert got == want
 
 

@@ -1,0 +1,142 @@
+"""Fused PPO minibatch gradient (csrc/learner.hip, quad_ppo_grad) against torch autograd of the
+SB3 loss (ppo/ppo.py `ppo_loss`) evaluated in float64 on a float64 copy of the same policy.
+
+Tolerance: the kernel sums B per-row terms in fp32 (MFMA k-chains, then a block-order sum of the
+per-block partials), so every gradient tensor must agree with the float64 gradient to
+|d| <= 1e-4 * max|g_ref| + 4 * err_torch32 and to |d| <= 4 * err_torch32 + 1e-6 * max|g_ref|, where
+err_torch32 is the error of torch's own fp32 autograd on the same inputs (a strongly cancelling sum
+over 262,144 rows has max|g| far below the sum of |terms|, so torch's error sets the scale there).
+Ratios are placed at least 1e-3 away from the clip bounds so that no implementation's rounding can
+flip a clipping decision; the exact in-range tie of min(A r, A clip(r)) follows torch (half the
+gradient to each side). Loss statistics to 1e-4 relative.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _policy(seed):
+    from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
+    torch.manual_seed(seed)
+    pol = ActorCritic(12, 4, (128, 128)).cuda()
+    with torch.no_grad():  # non-trivial biases / heads / log_std (orthogonal init leaves zeros)
+        for n, p in pol.named_parameters():
+            if n.endswith("bias"):
+                p.copy_(torch.randn_like(p) * 0.1)
+        pol.action_net.weight.mul_(30.0)
+        pol.log_std.copy_(torch.tensor([-0.4, 0.1, 0.3, -1.0]))
+    return pol
+
+
+def _buffers(pol, M, seed, clip):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    obs = (torch.rand(M, 12, generator=g) * 2 - 1).cuda()
+    obs[::7] *= 0.01  # rows near the origin
+    with torch.no_grad():
+        mean, v = pol.forward_heads(obs)
+        act = mean + pol.log_std.exp() * torch.randn(M, 4, generator=g).cuda()
+        lp = pol.log_prob(mean, act).double()
+    # target ratios in [0.55, 1.45], at least 1e-3 away from 1 +- clip
+    r = torch.rand(M, generator=g, dtype=torch.float64) * 0.9 + 0.55
+    for edge in (1 - clip, 1 + clip):
+        near = (r - edge).abs() < 1e-3
+        r[near] = edge + torch.where(r[near] >= edge, 2e-3, -2e-3).double()
+    logp_old = (lp - torch.log(r.cuda())).float()
+    adv = (torch.randn(M, generator=g) * 2.0 + 0.3).cuda()
+    ret = (v + torch.randn(M, generator=g).cuda()).float()
+    return obs, act.contiguous(), logp_old, adv, ret
+
+
+def _torch_grads(pol, dtype, obs, act, logp_old, adv, ret, idx, cfg):
+    from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
+    from uav_reinforcement_learning_control_amd.ppo.ppo import ppo_loss
+    from uav_reinforcement_learning_control_amd.ppo.learner import _ordered
+    ref = ActorCritic(12, 4, (128, 128)).to(device=obs.device, dtype=dtype)
+    ref.load_state_dict({k: v.to(dtype) for k, v in pol.state_dict().items()})
+    sel = [t[idx].to(dtype) for t in (obs, act, logp_old, adv, ret)]
+    loss, pg, vf, ent, cf = ppo_loss(ref, *sel, cfg)
+    loss.backward()
+    return [p.grad.double() for p in _ordered(ref)], torch.stack([pg, vf, ent, cf]).detach().double()
+
+
+@pytest.mark.parametrize("M,B,norm,seed", [
+    (6000, 6000, True, 0),       # whole buffer, several blocks with ragged last rounds
+    (20000, 4096 + 17, True, 1),
+    (3000, 64, True, 2),         # exactly one round
+    (3000, 37, False, 3),        # one partial round, no advantage normalization
+    (500, 1, True, 4),           # batch 1: normalization skipped (SB3 len(adv) > 1)
+    (300000, 262144, True, 5),   # many rounds per block, the 128-block cap
+])
+def test_fused_grad_matches_autograd(M, B, norm, seed):
+    from uav_reinforcement_learning_control_amd.ppo.learner import FusedLearner, _ordered
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig
+    cfg = PPOConfig(normalize_advantage=norm)
+    pol = _policy(seed)
+    obs, act, logp_old, adv, ret = _buffers(pol, M, seed, cfg.clip_range)
+    idx = torch.randperm(M, generator=torch.Generator().manual_seed(seed + 9))[:B].cuda()
+    fl = FusedLearner(pol, cfg.clip_range, cfg.ent_coef, cfg.vf_coef, norm)
+    for p in pol.parameters():  # garbage in .grad: the kernel must overwrite, not accumulate
+        p.grad = torch.full_like(p, 7.0)
+    stats = torch.zeros(4, device="cuda")
+    fl.grads(obs, act, logp_old, adv, ret, idx, stats)
+    torch.cuda.synchronize()
+    got = [p.grad.double() for p in _ordered(pol)]
+    ref64, st64 = _torch_grads(pol, torch.float64, obs, act, logp_old, adv, ret, idx, cfg)
+    ref32, _ = _torch_grads(pol, torch.float32, obs, act, logp_old, adv, ret, idx, cfg)
+    names = ["pi_w0", "pi_b0", "pi_w1", "pi_b1", "act_w", "act_b", "vf_w0", "vf_b0", "vf_w1", "vf_b1",
+             "val_w", "val_b", "log_std"]
+    for n, g, r64, r32 in zip(names, got, ref64, ref32):
+        scale = r64.abs().max().item()
+        err = (g - r64).abs().max().item()
+        err32 = (r32 - r64).abs().max().item()
+        tol = 1e-4 * scale + 4 * err32 + 1e-9  # (long cancelling sums: torch fp32's own error sets the bar)
+        assert err <= tol, f"{n}: max err {err:.3e} > {tol:.3e} (scale {scale:.3e}, torch fp32 err {err32:.3e})"
+        assert err <= 4 * err32 + 1e-6 * scale + 1e-9, f"{n}: err {err:.3e} vs torch fp32 {err32:.3e}"
+    np.testing.assert_allclose(stats.double().cpu().numpy(), st64.cpu().numpy(), rtol=1e-4, atol=1e-7)
+
+
+def test_fused_grad_rejects_bad_arguments():
+    from uav_reinforcement_learning_control_amd import _native as N
+    from uav_reinforcement_learning_control_amd.ppo.learner import FusedLearner
+    pol = _policy(0)
+    obs, act, logp_old, adv, ret = _buffers(pol, 100, 0, 0.2)
+    fl = FusedLearner(pol, 0.2, 0.0, 0.5)
+    with pytest.raises(ValueError):
+        fl.grads(obs, act, logp_old, adv, ret, torch.arange(10, device="cuda", dtype=torch.int32))
+    with pytest.raises(ValueError):
+        fl.grads(obs, act, logp_old, adv, ret, torch.arange(0, device="cuda"))
+    with pytest.raises(ValueError):
+        fl.grads(obs[:, :6].contiguous(), act, logp_old, adv, ret, torch.arange(10, device="cuda"))
+    L = N.lib()
+    assert L.quad_ppo_workspace_bytes(0) == 0
+    assert L.quad_ppo_grad(None, None, None, None, 0, None) == N.QUAD_EINVAL
+
+
+def test_ppo_train_fused_matches_torch_update():
+    """One PPO.train pass (2 minibatches) with the fused gradient vs the torch loss. Adam's first
+    steps move each parameter by ~lr * sign(g), so a gradient element within fp32 noise of zero
+    can move either way: allow that (<= 2 lr per step) on a small fraction of the elements, and
+    fp32 noise elsewhere."""
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
+    outs = []
+    for fused in (True, False):
+        env = QuadVecEnv(1024, env="hover", device="cuda:0", seed=3)
+        cfg = PPOConfig(n_steps=16, n_minibatches=2, n_epochs=1, fused_update=fused)
+        algo = PPO(env, cfg, seed=11)
+        algo.collect_rollouts()
+        torch.manual_seed(5)  # same epoch permutation
+        st = algo.train()
+        outs.append(([p.detach().clone() for p in algo.policy.parameters()], st))
+        env.close()
+    (pa, sa), (pb, sb) = outs
+    lr, steps = PPOConfig().learning_rate, 2
+    d = torch.cat([(a - b).abs().reshape(-1) for a, b in zip(pa, pb)])
+    assert d.max().item() <= 2 * lr * steps + 1e-6
+    assert (d > 1e-6).float().mean().item() < 0.01, f"{(d > 1e-6).sum().item()} of {d.numel()} differ"
+    for k in ("pg_loss", "vf_loss", "entropy", "clip_fraction"):
+        assert math.isclose(sa[k], sb[k], rel_tol=1e-3, abs_tol=1e-6), (k, sa[k], sb[k])

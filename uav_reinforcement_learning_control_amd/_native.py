@@ -15,7 +15,7 @@ CSRC = os.path.join(_PKG, "csrc")
 QUAD_OK, QUAD_EINVAL, QUAD_EHIP, QUAD_ENOMEM, QUAD_EMODEL = 0, -1, -2, -3, -4
 ENV_HOVER, ENV_TRAJ, ENV_BRAX_HOVER, ENV_BRAX_TRAJ = 0, 1, 2, 3
 WRAP_NONE, WRAP_CTBR, WRAP_RELPOS = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class QuadCfg(C.Structure):
@@ -95,7 +95,7 @@ EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_crea
            "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
            "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
            "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
-           "quad_waypoints_begin", "quad_waypoints_update")
+           "quad_waypoints_begin", "quad_waypoints_update", "quad_ppo_workspace_bytes", "quad_ppo_grad")
 
 
 class QuadRollout(C.Structure):
@@ -104,6 +104,18 @@ class QuadRollout(C.Structure):
                                           "stats")] + \
                [("rows", C.c_int32), ("t0", C.c_int32), ("steps", C.c_int32), ("deterministic", C.c_int32),
                 ("seed", C.c_uint64), ("gamma", C.c_float)]
+
+
+class QuadPolicyGrads(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("pi_w0", "pi_b0", "pi_w1", "pi_b1", "act_w", "act_b",
+                                          "vf_w0", "vf_b0", "vf_w1", "vf_b1", "val_w", "val_b",
+                                          "log_std")]
+
+
+class QuadPPOBatch(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("obs", "actions", "log_prob", "advantages", "returns", "index")] + \
+               [("batch", C.c_int32), ("normalize_advantage", C.c_int32), ("clip_range", C.c_float),
+                ("ent_coef", C.c_float), ("vf_coef", C.c_float), ("stats", C.c_void_p)]
 
 
 class QuadError(RuntimeError):
@@ -141,7 +153,11 @@ def _declare(L):
     L.quad_waypoints_begin.argtypes = [vp, C.POINTER(QuadWaypoints), C.POINTER(QuadWaypointState), vp, vp]
     L.quad_waypoints_update.argtypes = [vp, C.POINTER(QuadWaypoints), C.POINTER(QuadWaypointState),
                                         vp, vp, vp, vp, vp]
-    for n in ("quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
+    L.quad_ppo_workspace_bytes.argtypes = [i32]
+    L.quad_ppo_workspace_bytes.restype = C.c_int64
+    L.quad_ppo_grad.argtypes = [C.POINTER(QuadPolicyParams), C.POINTER(QuadPPOBatch), C.POINTER(QuadPolicyGrads),
+                                vp, C.c_int64, vp]
+    for n in ("quad_ppo_grad", "quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
               "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
               "quad_waypoints_begin", "quad_waypoints_update"):

@@ -31,12 +31,16 @@ def _need(t: torch.Tensor, shape, dtype, dev, name):
 class FusedPolicy:
     """Packed fp32 image of an ActorCritic (12 -> 128 -> 128 -> 4 / 1) for the MFMA kernels."""
 
-    def __init__(self, policy: ActorCritic):
+    @staticmethod
+    def _check_shapes(policy: ActorCritic) -> None:
         ex = policy.mlp_extractor
         shapes = [tuple(l.weight.shape) for l in (ex.policy_net[0], ex.policy_net[2], ex.value_net[0],
                                                   ex.value_net[2], policy.action_net, policy.value_net)]
         if shapes != [(128, 12), (128, 128), (128, 12), (128, 128), (4, 128), (1, 128)]:
-            raise ValueError(f"the MFMA policy kernel is built for 12-128-128-(4|1) nets, got {shapes}")
+            raise ValueError(f"the MFMA policy kernels are built for 12-128-128-(4|1) nets, got {shapes}")
+
+    def __init__(self, policy: ActorCritic):
+        self._check_shapes(policy)
         self.policy = policy
         self.device = policy.log_std.device
         if self.device.type != "cuda":

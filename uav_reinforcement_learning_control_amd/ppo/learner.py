@@ -1,0 +1,87 @@
+"""The PPO minibatch gradient on MFMA (csrc/learner.hip via quad_ppo_grad), bound to a torch
+ActorCritic.
+
+SB3 PPO.train (the learner the reference's train.py:50-68 configures; ppo/ppo.py `ppo_loss` restates
+its loss) computes, per minibatch, the clipped-surrogate + entropy + value loss and backpropagates it
+through both MLPs. `FusedLearner.grads` writes that gradient straight into the parameters' `.grad`
+tensors in three launches (advantage statistics, the fused forward/backward of both nets, a
+deterministic reduction of the per-block partials), gathering the minibatch rows from the rollout
+buffer through the permutation slice -- no minibatch copies, no autograd graph. The optimizer
+(gradient all-reduce, norm clip, Adam) then runs unchanged on `.grad`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from .. import _native as N
+from .fused import FusedPolicy, _need
+from .policy import ActorCritic
+
+
+def _ordered(policy: ActorCritic):
+    ex = policy.mlp_extractor
+    return [ex.policy_net[0].weight, ex.policy_net[0].bias, ex.policy_net[2].weight, ex.policy_net[2].bias,
+            policy.action_net.weight, policy.action_net.bias,
+            ex.value_net[0].weight, ex.value_net[0].bias, ex.value_net[2].weight, ex.value_net[2].bias,
+            policy.value_net.weight, policy.value_net.bias, policy.log_std]
+
+
+class FusedLearner:
+    """quad_ppo_grad for a 12-128-128-(4|1) ActorCritic (SB3 PPO loss semantics)."""
+
+    def __init__(self, policy: ActorCritic, clip_range: float, ent_coef: float, vf_coef: float,
+                 normalize_advantage: bool = True):
+        FusedPolicy._check_shapes(policy)
+        self.policy = policy
+        self.device = policy.log_std.device
+        if self.device.type != "cuda":
+            raise N.QuadError("FusedLearner needs the policy on a ROCm GPU")
+        self.clip_range, self.ent_coef, self.vf_coef = float(clip_range), float(ent_coef), float(vf_coef)
+        self.normalize_advantage = bool(normalize_advantage)
+        self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self._lib = N.lib()
+
+    def _structs(self):
+        ps = _ordered(self.policy)
+        for p in ps:
+            if not p.is_contiguous() or p.dtype != torch.float32:
+                raise ValueError("policy parameters must be contiguous float32")
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            elif not p.grad.is_contiguous():
+                raise ValueError("parameter gradients must be contiguous")
+        return (N.QuadPolicyParams(*[p.data_ptr() for p in ps]),
+                N.QuadPolicyGrads(*[p.grad.data_ptr() for p in ps]))
+
+    def grads(self, obs: torch.Tensor, actions: torch.Tensor, log_prob: torch.Tensor, advantages: torch.Tensor,
+              returns: torch.Tensor, index: torch.Tensor, stats: Optional[torch.Tensor] = None) -> None:
+        """Overwrite every parameter's .grad with the gradient of the PPO loss on rows `index` of the
+        flattened buffers (obs [M,12], actions [M,4], log_prob / advantages / returns [M]).
+        `stats` (float32 [4], optional) receives pg_loss, vf_loss, entropy, clip_fraction."""
+        dev = self.device
+        M = obs.shape[0]
+        _need(obs, (M, 12), torch.float32, dev, "obs")
+        _need(actions, (M, 4), torch.float32, dev, "actions")
+        for t, n in ((log_prob, "log_prob"), (advantages, "advantages"), (returns, "returns")):
+            _need(t, (M,), torch.float32, dev, n)
+        if index.dtype != torch.int64 or index.dim() != 1 or not index.is_contiguous() or index.device != dev:
+            raise ValueError("index: expected a contiguous int64 vector on the policy's device")
+        B = int(index.numel())
+        if B < 1:
+            raise ValueError("empty minibatch")
+        if stats is not None:
+            _need(stats, (4,), torch.float32, dev, "stats")
+        need = int(self._lib.quad_ppo_workspace_bytes(B))
+        if self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        prm, grd = self._structs()
+        b = N.QuadPPOBatch(obs.data_ptr(), actions.data_ptr(), log_prob.data_ptr(), advantages.data_ptr(),
+                           returns.data_ptr(), index.data_ptr(), B, int(self.normalize_advantage),
+                           self.clip_range, self.ent_coef, self.vf_coef,
+                           None if stats is None else stats.data_ptr())
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        N.check(self._lib.quad_ppo_grad(C.byref(prm), C.byref(b), C.byref(grd), C.c_void_p(self._ws.data_ptr()),
+                                        C.c_int64(self._ws.numel()), stream), "quad_ppo_grad")

@@ -31,6 +31,7 @@ import torch.nn as nn
 from .. import _native as N
 from .fused import FusedPolicy, rollout_supported
 from .gae import gae
+from .learner import FusedLearner
 from .policy import ActorCritic
 
 
@@ -53,6 +54,7 @@ class PPOConfig:
     fused_policy: bool = True             # rollout policy on the MFMA kernels (ppo/fused.py)
     fused_rollout: bool = True            # whole rollout as quad_rollout launches (needs fused_policy)
     rollout_chunk: int = 1024             # steps per quad_rollout launch
+    fused_update: bool = True             # minibatch gradient on MFMA (ppo/learner.py, quad_ppo_grad)
 
 
 def ppo_loss(policy: ActorCritic, obs, act, logp_old, adv, ret, cfg: PPOConfig):
@@ -150,6 +152,10 @@ class PPO:
                                                self.ep_ret, self.ep_len, self._slots, T, self.cfg.gamma)
         # one launch per chunk of steps: policy + env + bootstrap + statistics (csrc/rollout.hip)
         self._one_launch = (self._fp is not None and self.cfg.fused_rollout and rollout_supported(env))
+        # the update's minibatch gradient as quad_ppo_grad launches (same fusability as the rollout)
+        self._learner = (FusedLearner(self.policy, self.cfg.clip_range, self.cfg.ent_coef, self.cfg.vf_coef,
+                                      self.cfg.normalize_advantage)
+                         if self.cfg.fused_update and fusable and self.device.type == "cuda" else None)
         self._t_host = 0  # running step counter of the one-launch path (keys the action noise)
         self._noise_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5851F42D4C957F2D) & (2**64 - 1)
 
@@ -298,8 +304,11 @@ class PPO:
         nmb = max(1, total // B)
         stats = dict(pg_loss=0.0, vf_loss=0.0, entropy=0.0, clip_fraction=0.0, n=0)
         acc = torch.zeros(4, dtype=torch.float64, device=self.device)
+        epochs = n_epochs if n_epochs is not None else cfg.n_epochs
+        if self._learner is not None:
+            return self._train_fused(obs, act, logp_old, adv_all, ret, B, nmb, epochs, max_minibatches, stats)
         done = 0
-        for _ in range(n_epochs if n_epochs is not None else cfg.n_epochs):
+        for _ in range(epochs):
             perm = torch.randperm(total, device=self.device)
             for m in range(nmb):
                 if max_minibatches is not None and done >= max_minibatches:
@@ -318,6 +327,31 @@ class PPO:
                                         ent.detach().double(), cf.double()])
                 done += 1
         a = (acc / max(done, 1)).tolist()
+        stats.update(pg_loss=a[0], vf_loss=a[1], entropy=a[2], clip_fraction=a[3], n=done)
+        return stats
+
+    def _train_fused(self, obs, act, logp_old, adv, ret, B, nmb, epochs, max_minibatches, stats) -> dict:
+        """PPO.train with the minibatch gradient from quad_ppo_grad (no autograd graph, no
+        minibatch copies); all-reduce, norm clip and Adam unchanged."""
+        cfg = self.cfg
+        total = obs.shape[0]
+        steps = epochs * nmb if max_minibatches is None else min(epochs * nmb, max_minibatches)
+        mstats = torch.zeros(max(steps, 1), 4, dtype=torch.float32, device=self.device)
+        done = 0
+        for _ in range(epochs):
+            if done >= steps:
+                break
+            perm = torch.randperm(total, device=self.device)
+            for m in range(nmb):
+                if done >= steps:
+                    break
+                self._learner.grads(obs, act, logp_old, adv, ret, perm[m * B:(m + 1) * B], mstats[done])
+                if self.world > 1:
+                    allreduce_mean_(self.params, self._flat, self.world)
+                nn.utils.clip_grad_norm_(self.params, cfg.max_grad_norm)
+                self.opt.step()
+                done += 1
+        a = mstats[:done].double().mean(0).tolist() if done else [0.0] * 4
         stats.update(pg_loss=a[0], vf_loss=a[1], entropy=a[2], clip_fraction=a[3], n=done)
         return stats
 
