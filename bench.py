@@ -200,6 +200,9 @@ def _end_to_end(env, args) -> dict:
     out = {"n_steps": cfg.n_steps, "n_epochs": cfg.n_epochs, "minibatches_per_epoch": cfg.n_minibatches,
            "minibatch": m.batch, "iterations": args.e2e_iters,
            "rollout_s": t_roll / args.e2e_iters, "train_s": t_train / args.e2e_iters,
+           "update_path": "quad_ppo_grad (fused fwd+loss+bwd on MFMA) + clip + fused Adam"
+           if m._learner is not None else "torch autograd",
+           "ms_per_optimizer_step": 1e3 * t_train / args.e2e_iters / max(1, cfg.n_epochs * cfg.n_minibatches),
            "env_steps_per_s": steps / (t_roll + t_train)}
     del m
     torch.cuda.empty_cache()

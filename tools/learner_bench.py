@@ -17,6 +17,9 @@ def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 524288
     M = int(sys.argv[2]) if len(sys.argv) > 2 else 8 * 1024 * 1024
     iters = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    from uav_reinforcement_learning_control_amd import _native as N
+    if os.environ.get("QUADENV_LIB"):  # an ablation build (tools/learner_variants.sh)
+        N.LIB_PATH = os.environ["QUADENV_LIB"]
     from uav_reinforcement_learning_control_amd.ppo.learner import FusedLearner
     from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
     from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig, ppo_loss
@@ -66,6 +69,8 @@ def main():
 
     t = timed(fused_grad, iters)
     print(f"B={B} M={M}: quad_ppo_grad {t * 1e3:.1f} us  ({flop / t / 1e9:.1f} TF/s nominal)", flush=True)
+    if os.environ.get("QUADENV_LIB"):
+        return
     print(f"fused optimizer step {timed(fused_step, iters) * 1e3:.1f} us", flush=True)
     print(f"torch optimizer step {timed(torch_step, max(3, iters // 4)) * 1e3:.1f} us", flush=True)
 

@@ -227,6 +227,7 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
 #pragma unroll
     for (int r = 0; r < 16; r++) h2[0][r] = L[L_B2 + 32 * w + acc_row(r, h)];
     h2[1] = h2[0];
+#if !defined(QD_LRN_NOL2)  // QD_LRN_*: cost-ablation builds of tools/learner_variants.sh only
 #pragma unroll
     for (int m = 0; m < 32; m++) {
 #pragma unroll
@@ -236,6 +237,7 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
         h2[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(w2r[2 * m + 1], b.y, h2[t], 0, 0, 0);
       }
     }
+#endif
     // head partial sums over the wave's 32 neurons (the two lane halves hold 16 each)
     float part[2][NOUT];
 #pragma unroll
@@ -328,6 +330,7 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
     }
     __syncthreads();  // B4: DH2, H2 and dL/dmean images complete
 
+#if !defined(QD_LRN_NODW)
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows; db2 from the same A fragments
 #pragma unroll
     for (int s = 0; s < 32; s++) {
@@ -347,6 +350,8 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
       for (int b = 0; b < 2; b++)
         dW3[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, L[L_H2 + e * SH + 32 * w + 16 * b + k], dW3[b], 0, 0, 0);
     }
+#endif
+#if !defined(QD_LRN_NODH1)
     // ---- dh1 (R form) = relu'(h1) . (dh2 W2[:, block w]); then db1 and the dW1 slab
 #pragma unroll
     for (int t = 0; t < 2; t++) {
@@ -373,6 +378,7 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
         dW1 = __builtin_amdgcn_mfma_f32_32x32x2f32(acc[r], b, dW1, 0, 0, 0);
       }
     }
+#endif
   }
 
   // ---- block partials in the parameter layout
