@@ -472,7 +472,15 @@ __global__ __launch_bounds__(256) void k_ppo_reduce(RArgs a) {
   const int net = q / PSTRIDE, p = q % PSTRIDE;
   const float* src = a.part + size_t(net) * a.nb * PSTRIDE + p;
   float s = 0.f;
-  for (int b = 0; b < a.nb; b++) s += src[size_t(b) * PSTRIDE];
+  int b = 0;
+  for (; b + 16 <= a.nb; b += 16) {  // 16 loads in flight per thread; summed in block order
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = src[size_t(b + u) * PSTRIDE];
+#pragma unroll
+    for (int u = 0; u < 16; u++) s += v[u];
+  }
+  for (; b < a.nb; b++) s += src[size_t(b) * PSTRIDE];
   const QuadPolicyGrads& g = a.gr;
   if (p < P_B1) { (net ? g.vf_w0 : g.pi_w0)[p - P_W1] = s; return; }
   if (p < P_W2) { (net ? g.vf_b0 : g.pi_b0)[p - P_B1] = s; return; }
