@@ -6,7 +6,7 @@
 // path (ppo/ppo.py + policy._SplitKLinear) runs at ~30 TF/s. This file computes the whole minibatch
 // gradient of both nets in one launch (plus a stats pre-pass and a partial-sum reduction).
 //
-// Work split. One 256-thread block per CU works on ONE net (blocks [0, nb) the actor, [nb, 2nb)
+// Work split. One 256-thread block per CU works on ONE net (blocks [0, nb) the actor, [nb, nb + nbc)
 // the critic) over a contiguous slice of the minibatch, in rounds of 64 rows (two 32-row tiles).
 // Wave w owns neurons 32w..32w+31 of BOTH hidden layers, so its rows of W2 and its columns of W2
 // stay in registers for the whole launch (128 VGPRs of MFMA A/B fragments) and each wave
@@ -47,7 +47,11 @@ constexpr int RND = 64;       // rows per round (two 32-row MFMA tiles)
 constexpr int SH = 130;       // row stride (floats) of the [row][neuron] images
 constexpr int SO = 13;        // row stride of the observation image (odd: conflict-free columns)
 constexpr int ADV_BLOCKS = 256;
-constexpr int MAX_NB = 128;   // blocks per net (the device has 256 CUs)
+constexpr int MAX_NB = 128;   // blocks per net on average (the device has 256 CUs)
+#ifndef QD_LRN_ACTOR_SHARE
+#define QD_LRN_ACTOR_SHARE 540  // measured: 500 -> 1.30 ms, 525 -> 1.26, 540 -> 1.22-1.25, 550 -> 1.23, 580 -> 1.32
+#endif
+constexpr int ACTOR_SHARE = QD_LRN_ACTOR_SHARE;  // per mille of the block slots that run the actor
 
 // LDS image (floats)
 constexpr int L_H1 = 0, L_DH2 = L_H1 + RND * SH, L_H2 = L_DH2 + RND * SH;
@@ -79,8 +83,9 @@ struct GArgs {
   const float *obs, *act, *logp_old, *adv, *ret;
   const int64_t* idx;
   const double* adv_part;  // [ADV_BLOCKS][2] or NULL (no normalization)
-  float* part;             // [2 nb][PSTRIDE]
-  int32_t batch, nb, per_block;
+  float* part;             // [nb + nbc][PSTRIDE]: actor blocks, then critic blocks
+  int32_t batch, nb, per_block;     // actor: nb blocks of per_block rows
+  int32_t nbc, per_block_c;         // critic: nbc blocks of per_block_c rows
   float clip, inv_batch, vf_coef;
 };
 
@@ -157,8 +162,9 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
   for (int k = 0; k < ACT; k++) dls[k] = 0.f;
   const bool acc_lane = w == 0 && h == 0;  // one lane per row accumulates the per-row sums
 
-  const int s0 = blk * g.per_block;
-  const int s1 = min(g.batch, s0 + g.per_block);
+  const int per_block = NOUT == ACT ? g.per_block : g.per_block_c;
+  const int s0 = blk * per_block;
+  const int s1 = min(g.batch, s0 + per_block);
   const int rounds = s1 > s0 ? (s1 - s0 + RND - 1) / RND : 0;
   // Row staging, one round ahead: threads 0..191 gather the observation rows (float4 each),
   // threads 192..255 the row scalars; the minibatch indices are loaded two rounds ahead, so no
@@ -461,7 +467,7 @@ struct RArgs {
   const float* part;
   const float* log_std;
   float* stats;
-  int32_t nb;
+  int32_t nb, nbc;
   float inv_batch, ent_coef;
 };
 
@@ -471,16 +477,17 @@ __global__ __launch_bounds__(256) void k_ppo_reduce(RArgs a) {
   if (q >= 2 * PSTRIDE) return;
   const int net = q / PSTRIDE, p = q % PSTRIDE;
   const float* src = a.part + size_t(net) * a.nb * PSTRIDE + p;
+  const int nb = net ? a.nbc : a.nb;
   float s = 0.f;
   int b = 0;
-  for (; b + 16 <= a.nb; b += 16) {  // 16 loads in flight per thread; summed in block order
+  for (; b + 16 <= nb; b += 16) {  // 16 loads in flight per thread; summed in block order
     float v[16];
 #pragma unroll
     for (int u = 0; u < 16; u++) v[u] = src[size_t(b + u) * PSTRIDE];
 #pragma unroll
     for (int u = 0; u < 16; u++) s += v[u];
   }
-  for (; b < a.nb; b++) s += src[size_t(b) * PSTRIDE];
+  for (; b < nb; b++) s += src[size_t(b) * PSTRIDE];
   const QuadPolicyGrads& g = a.gr;
   if (p < P_B1) { (net ? g.vf_w0 : g.pi_w0)[p - P_W1] = s; return; }
   if (p < P_W2) { (net ? g.vf_b0 : g.pi_b0)[p - P_B1] = s; return; }
@@ -509,16 +516,23 @@ __global__ __launch_bounds__(256) void k_ppo_reduce(RArgs a) {
 int lfail(int code, const char* m) { return set_error(code, m); }
 
 struct Layout {
-  int nb, per_block;
+  int nb, per_block, nbc, per_block_c;
   int64_t part_bytes, adv_bytes;
 };
 
 Layout layout_of(int32_t batch) {
   Layout l{};
   const int rounds = (batch + RND - 1) / RND;
-  l.nb = rounds < MAX_NB ? rounds : MAX_NB;
+  // the critic's rows cost less than the actor's (no log-prob / ratio work): the two nets share
+  // the 2 * MAX_NB block slots in proportion to their measured round times (ACTOR_SHARE / 1000)
+  const int slots = rounds < MAX_NB ? 2 * rounds : 2 * MAX_NB;
+  int na = int((int64_t(slots) * ACTOR_SHARE + 500) / 1000);
+  na = na < 1 ? 1 : (na > slots - 1 ? slots - 1 : na);
+  l.nb = na < rounds ? na : rounds;
+  l.nbc = slots - na < rounds ? slots - na : rounds;
   l.per_block = ((rounds + l.nb - 1) / l.nb) * RND;
-  l.part_bytes = int64_t(2) * l.nb * PSTRIDE * int64_t(sizeof(float));
+  l.per_block_c = ((rounds + l.nbc - 1) / l.nbc) * RND;
+  l.part_bytes = int64_t(l.nb + l.nbc) * PSTRIDE * int64_t(sizeof(float));
   l.adv_bytes = int64_t(ADV_BLOCKS) * 2 * int64_t(sizeof(double));
   return l;
 }
@@ -580,12 +594,12 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   g.idx = b->index;
   g.adv_part = norm ? adv_part : nullptr;
   g.part = part;
-  g.batch = b->batch; g.nb = l.nb; g.per_block = l.per_block;
+  g.batch = b->batch; g.nb = l.nb; g.per_block = l.per_block; g.nbc = l.nbc; g.per_block_c = l.per_block_c;
   g.clip = b->clip_range; g.inv_batch = 1.0f / float(b->batch); g.vf_coef = b->vf_coef;
-  hipLaunchKernelGGL(k_ppo_grad, dim3(2 * l.nb), dim3(LB), lds_bytes, s, g);
+  hipLaunchKernelGGL(k_ppo_grad, dim3(l.nb + l.nbc), dim3(LB), lds_bytes, s, g);
   if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_grad launch failed");
   RArgs r{};
-  r.gr = *gr; r.part = part; r.log_std = p->log_std; r.stats = b->stats; r.nb = l.nb;
+  r.gr = *gr; r.part = part; r.log_std = p->log_std; r.stats = b->stats; r.nb = l.nb; r.nbc = l.nbc;
   r.inv_batch = 1.0f / float(b->batch); r.ent_coef = b->ent_coef;
   hipLaunchKernelGGL(k_ppo_reduce, dim3((2 * PSTRIDE + 255) / 256), dim3(256), 0, s, r);
   if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_reduce launch failed");
