@@ -338,7 +338,7 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
 
 #if !defined(QD_LRN_NODW)
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows; db2 from the same A fragments
-#pragma unroll
+#pragma unroll 8  // (measured: full 1.226 ms, 8 1.204, 4 1.208, 2 1.234)
     for (int s = 0; s < 32; s++) {
       const int e = 2 * s + h;
       const float a = L[L_DH2 + e * SH + n_own];
