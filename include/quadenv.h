@@ -351,6 +351,29 @@ typedef struct QuadPPOBatch {
   float* stats;             /* [4] out, or NULL: pg_loss, vf_loss, entropy, clip_fraction */
 } QuadPPOBatch;
 
+/* ---- The optimizer step of PPO.train (row P), fused: torch.nn.utils.clip_grad_norm_(params,
+ * max_grad_norm) followed by torch.optim.Adam.step() (SB3's policy optimizer, eps = 1e-5 in
+ * train.py's policy_kwargs) over up to QUAD_ADAM_MAX_TENSORS device fp32 tensors, in two launches:
+ *   total = ||all grads||_2; coef = min(max_grad_norm / (total + 1e-6), 1); grad *= coef
+ *   (skipped when max_grad_norm <= 0); step += 1; m = b1 m + (1 - b1) g; v = b2 v + (1 - b2) g^2;
+ *   p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps).
+ * `step` points at each tensor's step counter (torch's float32 state["step"]); all are incremented. */
+enum { QUAD_ADAM_MAX_TENSORS = 16 };
+typedef struct QuadAdam {
+  float* params[QUAD_ADAM_MAX_TENSORS];
+  float* grads[QUAD_ADAM_MAX_TENSORS];       /* clipped in place, as clip_grad_norm_ does */
+  float* exp_avg[QUAD_ADAM_MAX_TENSORS];
+  float* exp_avg_sq[QUAD_ADAM_MAX_TENSORS];
+  float* step[QUAD_ADAM_MAX_TENSORS];
+  int32_t numel[QUAD_ADAM_MAX_TENSORS];
+  int32_t count;                             /* tensors in use, 1..QUAD_ADAM_MAX_TENSORS */
+  float max_grad_norm;
+  double lr, beta1, beta2, eps;              /* moments and step size are formed in float64 */
+} QuadAdam;
+/* Device workspace (bytes) quad_clip_adam needs (gradient-norm partials). */
+int64_t quad_adam_workspace_bytes(const QuadAdam* a);
+int quad_clip_adam(const QuadAdam* a, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* Device workspace (bytes) quad_ppo_grad needs for a minibatch of `batch` rows. */
 int64_t quad_ppo_workspace_bytes(int32_t batch);
 int quad_ppo_grad(const QuadPolicyParams* params, const QuadPPOBatch* b, const QuadPolicyGrads* grads,

@@ -48,6 +48,7 @@ int main(void) {{
   printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(QuadPolicyParams), sizeof(QuadPolicyAct),
          offsetof(QuadPolicyAct, rows), offsetof(QuadPolicyAct, env_id_base),
          sizeof(QuadRolloutPost), offsetof(QuadRolloutPost, rows), offsetof(QuadRolloutPost, gamma));
+  printf("%zu %zu %zu\\n", sizeof(QuadAdam), offsetof(QuadAdam, max_grad_norm), offsetof(QuadAdam, eps));
   printf("%zu %zu %zu %zu %zu\\n", sizeof(QuadPolicyGrads), sizeof(QuadPPOBatch), offsetof(QuadPPOBatch, batch),
          offsetof(QuadPPOBatch, vf_coef), offsetof(QuadPPOBatch, stats));
   return 0;
@@ -60,6 +61,7 @@ int main(void) {{
             C.sizeof(N.QuadPolicyParams), C.sizeof(N.QuadPolicyAct), N.QuadPolicyAct.rows.offset,
             N.QuadPolicyAct.env_id_base.offset, C.sizeof(N.QuadRolloutPost),
             N.QuadRolloutPost.rows.offset, N.QuadRolloutPost.gamma.offset,
+            C.sizeof(N.QuadAdam), N.QuadAdam.max_grad_norm.offset, N.QuadAdam.eps.offset,
             C.sizeof(N.QuadPolicyGrads), C.sizeof(N.QuadPPOBatch), N.QuadPPOBatch.batch.offset,
             N.QuadPPOBatch.vf_coef.offset, N.QuadPPOBatch.stats.offset]
     assert got == want

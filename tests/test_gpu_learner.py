@@ -140,3 +140,35 @@ def test_ppo_train_fused_matches_torch_update():
     assert (d > 1e-6).float().mean().item() < 0.01, f"{(d > 1e-6).sum().item()} of {d.numel()} differ"
     for k in ("pg_loss", "vf_loss", "entropy", "clip_fraction"):
         assert math.isclose(sa[k], sb[k], rel_tol=1e-3, abs_tol=1e-6), (k, sa[k], sb[k])
+
+
+@pytest.mark.parametrize("max_norm", [0.5, 1e9, 0.0])
+def test_fused_clip_adam_matches_torch(max_norm):
+    """quad_clip_adam (clip_grad_norm_ + Adam.step) vs torch's on identical gradients, 4 steps, on
+    the optimizer's own state (step counters, moments): fp32 rounding-level agreement."""
+    from uav_reinforcement_learning_control_amd.ppo.learner import FusedAdam
+    pa, pb = _policy(7), _policy(7)
+    oa = torch.optim.Adam(pa.parameters(), lr=3e-3, eps=1e-5, fused=True)
+    ob = torch.optim.Adam(pb.parameters(), lr=3e-3, eps=1e-5, fused=True)
+    fa = FusedAdam(oa, max_norm)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    for it in range(4):
+        for p, q in zip(pa.parameters(), pb.parameters()):
+            gr = (torch.randn(p.shape, generator=g) * (3.0 if it % 2 else 0.01)).cuda()
+            p.grad = gr.clone()
+            q.grad = gr.clone()
+        fa.step()
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(list(pb.parameters()), max_norm)
+        ob.step()
+    torch.cuda.synchronize()
+    for (n, p), q in zip(pa.named_parameters(), pb.parameters()):
+        d = (p - q).abs().max().item()
+        assert d <= 1e-6 * max(1.0, q.abs().max().item()), (n, d)
+        assert torch.allclose(p.grad, q.grad, rtol=1e-5, atol=1e-8), n  # clipped in place as torch does
+        sa, sb = oa.state[p], ob.state[q]
+        assert float(sa["step"]) == float(sb["step"]) == 4.0
+        assert torch.allclose(sa["exp_avg"], sb["exp_avg"], rtol=1e-5, atol=1e-9), n
+        assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-12), n
+    # the optimizer state stays torch's: a plain torch step continues from it
+    oa.step()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Profiling tool (not product): one PPO minibatch optimizer step at the SB3 schedule's size
 (524,288 rows of a 65,536 x 1,024 buffer) -- quad_ppo_grad alone, the fused optimizer step
-(gradient + norm clip + fused Adam), and the torch autograd step (ppo_loss + backward + clip +
+(quad_ppo_grad + quad_clip_adam), and the torch autograd step (ppo_loss + backward + clip +
 Adam), HIP-event timed. Usage: learner_bench.py [B] [M] [iters]"""
 import os
 import sys
@@ -20,7 +20,7 @@ def main():
     from uav_reinforcement_learning_control_amd import _native as N
     if os.environ.get("QUADENV_LIB"):  # an ablation build (tools/learner_variants.sh)
         N.LIB_PATH = os.environ["QUADENV_LIB"]
-    from uav_reinforcement_learning_control_amd.ppo.learner import FusedLearner
+    from uav_reinforcement_learning_control_amd.ppo.learner import FusedAdam, FusedLearner
     from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
     from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig, ppo_loss
     torch.manual_seed(0)
@@ -36,6 +36,7 @@ def main():
     params = list(pol.parameters())
     opt = torch.optim.Adam(params, lr=cfg.learning_rate, eps=cfg.adam_eps, fused=True)
     fl = FusedLearner(pol, cfg.clip_range, cfg.ent_coef, cfg.vf_coef)
+    fadam = FusedAdam(opt, cfg.max_grad_norm)
     stats = torch.zeros(4, device="cuda")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     flop = 2 * B * (2 * (12 * 128 + 128 * 128) + 5 * 128) * 3  # fwd + 2x bwd, both nets
@@ -56,8 +57,7 @@ def main():
 
     def fused_step():
         fused_grad()
-        torch.nn.utils.clip_grad_norm_(params, cfg.max_grad_norm)
-        opt.step()
+        fadam.step()  # quad_clip_adam
 
     def torch_step():
         idx = torch.randint(0, M, (B,), device="cuda")

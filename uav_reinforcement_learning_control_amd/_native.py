@@ -95,7 +95,8 @@ EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_crea
            "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
            "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
            "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
-           "quad_waypoints_begin", "quad_waypoints_update", "quad_ppo_workspace_bytes", "quad_ppo_grad")
+           "quad_waypoints_begin", "quad_waypoints_update", "quad_ppo_workspace_bytes", "quad_ppo_grad",
+           "quad_adam_workspace_bytes", "quad_clip_adam")
 
 
 class QuadRollout(C.Structure):
@@ -116,6 +117,15 @@ class QuadPPOBatch(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("obs", "actions", "log_prob", "advantages", "returns", "index")] + \
                [("batch", C.c_int32), ("normalize_advantage", C.c_int32), ("clip_range", C.c_float),
                 ("ent_coef", C.c_float), ("vf_coef", C.c_float), ("stats", C.c_void_p)]
+
+
+ADAM_MAX_TENSORS = 16
+
+
+class QuadAdam(C.Structure):
+    _fields_ = [(n, C.c_void_p * ADAM_MAX_TENSORS) for n in ("params", "grads", "exp_avg", "exp_avg_sq", "step")] + \
+               [("numel", C.c_int32 * ADAM_MAX_TENSORS), ("count", C.c_int32), ("max_grad_norm", C.c_float),
+                ("lr", C.c_double), ("beta1", C.c_double), ("beta2", C.c_double), ("eps", C.c_double)]
 
 
 class QuadError(RuntimeError):
@@ -157,7 +167,10 @@ def _declare(L):
     L.quad_ppo_workspace_bytes.restype = C.c_int64
     L.quad_ppo_grad.argtypes = [C.POINTER(QuadPolicyParams), C.POINTER(QuadPPOBatch), C.POINTER(QuadPolicyGrads),
                                 vp, C.c_int64, vp]
-    for n in ("quad_ppo_grad", "quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
+    L.quad_adam_workspace_bytes.argtypes = [C.POINTER(QuadAdam)]
+    L.quad_adam_workspace_bytes.restype = C.c_int64
+    L.quad_clip_adam.argtypes = [C.POINTER(QuadAdam), vp, C.c_int64, vp]
+    for n in ("quad_clip_adam", "quad_ppo_grad", "quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
               "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
               "quad_waypoints_begin", "quad_waypoints_update"):

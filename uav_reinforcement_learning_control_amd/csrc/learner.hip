@@ -537,6 +537,90 @@ Layout layout_of(int32_t batch) {
   return l;
 }
 
+
+// ---- fused clip_grad_norm_ + Adam (quad_clip_adam)
+constexpr int ADAM_BLOCK = 256;
+
+struct AdamArgs {
+  QuadAdam a;
+  int32_t offs[QUAD_ADAM_MAX_TENSORS + 1];  // prefix sums of numel
+  float* part;                              // [nblocks] sums of squares
+  int32_t nblocks;
+};
+
+__device__ __forceinline__ int tensor_of(const AdamArgs& g, int i) {
+  int t = 0;
+#pragma unroll
+  for (int k = 1; k < QUAD_ADAM_MAX_TENSORS; k++) t += (k < g.a.count && i >= g.offs[k]) ? 1 : 0;
+  return t;
+}
+
+// per-block sums of squared gradients (fixed-order tree); block 0 advances the step counters
+__global__ __launch_bounds__(ADAM_BLOCK) void k_grad_sumsq(AdamArgs g) {
+  __shared__ float red[ADAM_BLOCK];
+  const int i = blockIdx.x * ADAM_BLOCK + threadIdx.x;
+  float v = 0.f;
+  if (i < g.offs[g.a.count]) {
+    const int t = tensor_of(g, i);
+    const float x = g.a.grads[t][i - g.offs[t]];
+    v = x * x;
+  }
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = ADAM_BLOCK / 2; o > 0; o >>= 1) {
+    if (int(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) g.part[blockIdx.x] = red[0];
+  if (blockIdx.x == 0 && int(threadIdx.x) < g.a.count) g.a.step[threadIdx.x][0] += 1.f;
+}
+
+// every block reduces the partials in the same order (same norm everywhere), then clips + updates
+__global__ __launch_bounds__(ADAM_BLOCK) void k_adam(AdamArgs g) {
+  __shared__ float red[ADAM_BLOCK];
+  float v = 0.f;
+  for (int b = threadIdx.x; b < g.nblocks; b += ADAM_BLOCK) v += g.part[b];
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = ADAM_BLOCK / 2; o > 0; o >>= 1) {
+    if (int(threadIdx.x) < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  const int i = blockIdx.x * ADAM_BLOCK + threadIdx.x;
+  if (i >= g.offs[g.a.count]) return;
+  const int t = tensor_of(g, i), j = i - g.offs[t];
+  float gr = g.a.grads[t][j];
+  if (g.a.max_grad_norm > 0.f) {
+    const float coef = fminf(g.a.max_grad_norm / (sqrtf(red[0]) + 1e-6f), 1.f);
+    gr *= coef;
+    g.a.grads[t][j] = gr;
+  }
+  const double step = g.a.step[t][0];
+  const double b1 = g.a.beta1, b2 = g.a.beta2, gd = gr;
+  const float m = float(b1 * double(g.a.exp_avg[t][j]) + (1.0 - b1) * gd);
+  const float vv = float(b2 * double(g.a.exp_avg_sq[t][j]) + (1.0 - b2) * gd * gd);
+  g.a.exp_avg[t][j] = m;
+  g.a.exp_avg_sq[t][j] = vv;
+  const double bc1 = 1.0 - pow(b1, step), bc2 = 1.0 - pow(b2, step);
+  const double denom = sqrt(double(vv)) / sqrt(bc2) + g.a.eps;
+  g.a.params[t][j] = float(double(g.a.params[t][j]) - (g.a.lr / bc1) * double(m) / denom);
+}
+
+int adam_layout(const QuadAdam* a, AdamArgs& g) {
+  if (!a || a->count < 1 || a->count > QUAD_ADAM_MAX_TENSORS) return lfail(QUAD_EINVAL, "count out of range");
+  g.a = *a;
+  g.offs[0] = 0;
+  for (int t = 0; t < a->count; t++) {
+    if (!a->params[t] || !a->grads[t] || !a->exp_avg[t] || !a->exp_avg_sq[t] || !a->step[t])
+      return lfail(QUAD_EINVAL, "a tensor pointer is NULL");
+    if (a->numel[t] < 1) return lfail(QUAD_EINVAL, "numel must be >= 1");
+    if (int64_t(g.offs[t]) + a->numel[t] > (int64_t(1) << 30)) return lfail(QUAD_EINVAL, "too many elements");
+    g.offs[t + 1] = g.offs[t] + a->numel[t];
+  }
+  for (int t = a->count; t < QUAD_ADAM_MAX_TENSORS; t++) g.offs[t + 1] = g.offs[a->count];
+  g.nblocks = (g.offs[a->count] + ADAM_BLOCK - 1) / ADAM_BLOCK;
+  return QUAD_OK;
+}
 }  // namespace
 }  // namespace quadenv
 
@@ -603,6 +687,28 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   r.inv_batch = 1.0f / float(b->batch); r.ent_coef = b->ent_coef;
   hipLaunchKernelGGL(k_ppo_reduce, dim3((2 * PSTRIDE + 255) / 256), dim3(256), 0, s, r);
   if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_reduce launch failed");
+  return QUAD_OK;
+}
+
+int64_t quad_adam_workspace_bytes(const QuadAdam* a) {
+  AdamArgs g{};
+  if (adam_layout(a, g) != QUAD_OK) return 0;
+  return int64_t(g.nblocks) * int64_t(sizeof(float));
+}
+
+int quad_clip_adam(const QuadAdam* a, void* workspace, int64_t workspace_bytes, void* stream) {
+  AdamArgs g{};
+  if (int rc = adam_layout(a, g)) return rc;
+  if (!workspace || workspace_bytes < int64_t(g.nblocks) * int64_t(sizeof(float)))
+    return lfail(QUAD_EINVAL, "workspace too small");
+  if (!(a->eps > 0.0) || !(a->lr >= 0.0) || !(a->beta1 >= 0.0 && a->beta1 < 1.0) || !(a->beta2 >= 0.0 && a->beta2 < 1.0))
+    return lfail(QUAD_EINVAL, "need lr >= 0, eps > 0, 0 <= betas < 1");
+  g.part = static_cast<float*>(workspace);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(k_grad_sumsq, dim3(g.nblocks), dim3(ADAM_BLOCK), 0, s, g);
+  if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_grad_sumsq launch failed");
+  hipLaunchKernelGGL(k_adam, dim3(g.nblocks), dim3(ADAM_BLOCK), 0, s, g);
+  if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_adam launch failed");
   return QUAD_OK;
 }
 

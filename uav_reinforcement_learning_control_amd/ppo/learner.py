@@ -6,8 +6,9 @@ its loss) computes, per minibatch, the clipped-surrogate + entropy + value loss 
 through both MLPs. `FusedLearner.grads` writes that gradient straight into the parameters' `.grad`
 tensors in three launches (advantage statistics, the fused forward/backward of both nets, a
 deterministic reduction of the per-block partials), gathering the minibatch rows from the rollout
-buffer through the permutation slice -- no minibatch copies, no autograd graph. The optimizer
-(gradient all-reduce, norm clip, Adam) then runs unchanged on `.grad`.
+buffer through the permutation slice -- no minibatch copies, no autograd graph. After the
+(multi-GPU) gradient all-reduce, `FusedAdam.step` does clip_grad_norm_ + Adam.step in two launches
+on torch's own optimizer state.
 """
 from __future__ import annotations
 
@@ -85,3 +86,65 @@ class FusedLearner:
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         N.check(self._lib.quad_ppo_grad(C.byref(prm), C.byref(b), C.byref(grd), C.c_void_p(self._ws.data_ptr()),
                                         C.c_int64(self._ws.numel()), stream), "quad_ppo_grad")
+
+
+def adam_state(opt: torch.optim.Adam, params) -> list:
+    """torch.optim.Adam's per-parameter state (step, exp_avg, exp_avg_sq), created the way Adam's
+    first step() does (fused/capturable: the step counter is a float32 tensor on the device)."""
+    out = []
+    for p in params:
+        st = opt.state[p]
+        if len(st) == 0:
+            st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        if st["step"].device != p.device:
+            st["step"] = st["step"].to(device=p.device, dtype=torch.float32)
+        out.append(st)
+    return out
+
+
+class FusedAdam:
+    """clip_grad_norm_(params, max_grad_norm) + opt.step() for a torch.optim.Adam as two launches
+    (quad_clip_adam), on the optimizer's own state tensors so state_dict()/checkpoints are unchanged."""
+
+    def __init__(self, opt: torch.optim.Adam, max_grad_norm: float):
+        if len(opt.param_groups) != 1:
+            raise ValueError("FusedAdam expects one parameter group")
+        grp = opt.param_groups[0]
+        if grp.get("amsgrad") or grp.get("maximize") or grp.get("weight_decay", 0.0) != 0.0:
+            raise ValueError("FusedAdam implements plain Adam (no amsgrad / maximize / weight decay)")
+        self.opt, self.params = opt, list(grp["params"])
+        if len(self.params) > N.ADAM_MAX_TENSORS:
+            raise ValueError("too many parameter tensors")
+        for p in self.params:
+            if p.dtype != torch.float32 or not p.is_contiguous() or p.device.type != "cuda":
+                raise ValueError("parameters must be contiguous float32 on a ROCm GPU")
+        self.max_grad_norm = float(max_grad_norm)
+        self._lib = N.lib()
+        self._ws = None
+
+    def _build(self):
+        grp = self.opt.param_groups[0]
+        st = adam_state(self.opt, self.params)
+        a = N.QuadAdam()
+        for i, (p, s) in enumerate(zip(self.params, st)):
+            if p.grad is None or not p.grad.is_contiguous():
+                raise ValueError("every parameter needs a contiguous .grad")
+            a.params[i], a.grads[i] = p.data_ptr(), p.grad.data_ptr()
+            a.exp_avg[i], a.exp_avg_sq[i], a.step[i] = (s["exp_avg"].data_ptr(), s["exp_avg_sq"].data_ptr(),
+                                                        s["step"].data_ptr())
+            a.numel[i] = p.numel()
+        a.count = len(self.params)
+        b1, b2 = grp["betas"]
+        a.lr, a.beta1, a.beta2, a.eps, a.max_grad_norm = float(grp["lr"]), b1, b2, float(grp["eps"]), self.max_grad_norm
+        return a
+
+    def step(self) -> None:
+        a = self._build()
+        if self._ws is None:
+            self._ws = torch.empty(max(int(self._lib.quad_adam_workspace_bytes(C.byref(a))), 4), dtype=torch.uint8,
+                                   device=self.params[0].device)
+        stream = C.c_void_p(torch.cuda.current_stream(self.params[0].device).cuda_stream)
+        N.check(self._lib.quad_clip_adam(C.byref(a), C.c_void_p(self._ws.data_ptr()), C.c_int64(self._ws.numel()),
+                                         stream), "quad_clip_adam")

@@ -31,7 +31,7 @@ import torch.nn as nn
 from .. import _native as N
 from .fused import FusedPolicy, rollout_supported
 from .gae import gae
-from .learner import FusedLearner
+from .learner import FusedAdam, FusedLearner
 from .policy import ActorCritic
 
 
@@ -156,6 +156,7 @@ class PPO:
         self._learner = (FusedLearner(self.policy, self.cfg.clip_range, self.cfg.ent_coef, self.cfg.vf_coef,
                                       self.cfg.normalize_advantage)
                          if self.cfg.fused_update and fusable and self.device.type == "cuda" else None)
+        self._adam = FusedAdam(self.opt, self.cfg.max_grad_norm) if self._learner is not None else None
         self._t_host = 0  # running step counter of the one-launch path (keys the action noise)
         self._noise_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5851F42D4C957F2D) & (2**64 - 1)
 
@@ -332,7 +333,7 @@ class PPO:
 
     def _train_fused(self, obs, act, logp_old, adv, ret, B, nmb, epochs, max_minibatches, stats) -> dict:
         """PPO.train with the minibatch gradient from quad_ppo_grad (no autograd graph, no
-        minibatch copies); all-reduce, norm clip and Adam unchanged."""
+        minibatch copies), the flat-bucket all-reduce, then clip_grad_norm_ + Adam as quad_clip_adam."""
         cfg = self.cfg
         total = obs.shape[0]
         steps = epochs * nmb if max_minibatches is None else min(epochs * nmb, max_minibatches)
@@ -348,8 +349,7 @@ class PPO:
                 self._learner.grads(obs, act, logp_old, adv, ret, perm[m * B:(m + 1) * B], mstats[done])
                 if self.world > 1:
                     allreduce_mean_(self.params, self._flat, self.world)
-                nn.utils.clip_grad_norm_(self.params, cfg.max_grad_norm)
-                self.opt.step()
+                self._adam.step()  # clip_grad_norm_ + Adam.step (quad_clip_adam)
                 done += 1
         a = mstats[:done].double().mean(0).tolist() if done else [0.0] * 4
         stats.update(pg_loss=a[0], vf_loss=a[1], entropy=a[2], clip_fraction=a[3], n=done)
