@@ -79,7 +79,7 @@ int main() {
     const float t = run<false>(65536, 100, chain);
     printf("n=65536 chain=%d x4 FMAs: %.2f us\n", chain, t);
   }
-  for (int n : {65536, 262144, 1048576}) {
+  for (int n : {4096, 65536, 262144, 1048576}) {
     const float a = run<false>(n, 100), b = run<true>(n, 100);
     const double bytes = 278.0 * n;
     printf("n=%d plain %.2f us (%.0f GB/s)  write-through %.2f us (%.0f GB/s)\n", n, a, bytes / a / 1e3, b, bytes / b / 1e3);
