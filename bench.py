@@ -200,13 +200,41 @@ def _end_to_end(env, args) -> dict:
     out = {"n_steps": cfg.n_steps, "n_epochs": cfg.n_epochs, "minibatches_per_epoch": cfg.n_minibatches,
            "minibatch": m.batch, "iterations": args.e2e_iters,
            "rollout_s": t_roll / args.e2e_iters, "train_s": t_train / args.e2e_iters,
-           "update_path": "quad_ppo_grad (fused fwd+loss+bwd on MFMA) + clip + fused Adam"
+           "update_path": "quad_ppo_grad (fused fwd+loss+bwd on MFMA) + quad_clip_adam"
            if m._learner is not None else "torch autograd",
            "ms_per_optimizer_step": 1e3 * t_train / args.e2e_iters / max(1, cfg.n_epochs * cfg.n_minibatches),
            "env_steps_per_s": steps / (t_roll + t_train)}
+    if m._learner is not None:
+        out["learner_kernel"] = _learner_kernel(m)
     del m
     torch.cuda.empty_cache()
     return out
+
+
+def _learner_kernel(m) -> dict:
+    """quad_ppo_grad alone on the rollout buffer (one minibatch of the SB3 schedule), HIP-event
+    timed on its stream: the MFMA roofline of the update. FLOP = the issued 32x32x2 / 16x16x4
+    products per row (L1, L2, dW2, dh1, dW1 + the dW3 16x16x4) for both nets."""
+    total = m.buf_obs.shape[0] * m.buf_obs.shape[1]
+    obs, act = m.buf_obs.view(total, -1), m.buf_act.view(total, 4)
+    lp, adv, ret = m.buf_logp.view(total), m.buf_adv.view(total), m.buf_ret.view(total)
+    idx = torch.randperm(total, device=obs.device)[:m.batch].contiguous()
+    m._learner.grads(obs, act, lp, adv, ret, idx)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    e0.record()
+    for _ in range(reps):
+        m._learner.grads(obs, act, lp, adv, ret, idx)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    # issued MFMA work per row per net: (12 + 128 + 128 + 128 + 32) 32x32x2 per 64 rows per wave x 4
+    # waves, plus 32 16x16x4 (half the cycles) -> 444 x 2048 x 2 flop x 4 / 64 rows
+    flop = 2 * m.batch * (444 * 2048 * 2 * 4 / 64)
+    return {"kernel": "quad_ppo_grad (k_adv_stats + k_ppo_grad + k_ppo_reduce)", "rows": m.batch,
+            "us_per_minibatch": us, "issued_flop": flop, "achieved_TFLOPs": flop / us / 1e6,
+            "peak_TFLOPs": 157.3, "bound": "mfma (fp32 32x32x2)"}
 
 
 def _rollout_phase(env, args) -> dict:
