@@ -172,3 +172,48 @@ def test_fused_clip_adam_matches_torch(max_norm):
         assert torch.allclose(sa["exp_avg_sq"], sb["exp_avg_sq"], rtol=1e-5, atol=1e-12), n
     # the optimizer state stays torch's: a plain torch step continues from it
     oa.step()
+
+
+def _dp_worker(rank, world, port, q):
+    try:
+        import os
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # both ranks share cuda:0 here
+        from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+        from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
+        n = 2048
+        env = QuadVecEnv(n, env="hover", device="cuda:0", seed=5, env_id_base=rank * n)
+        algo = PPO(env, PPOConfig(n_steps=16, n_minibatches=4, n_epochs=1), seed=3)
+        assert algo._learner is not None and algo.world == world
+        p0 = torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()]).cpu()
+        algo.collect_rollouts()
+        st = algo.train()
+        p1 = torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()]).cpu()
+        q.put((rank, p0.numpy(), p1.numpy(), st["n"]))
+        env.close()
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of leaving the parent waiting
+        q.put((rank, repr(e), None, None))
+
+
+def test_fused_update_two_ranks_stay_in_sync():
+    """Data-parallel PPO with the fused update: 2 ranks (gloo, one GPU), different env shards,
+    one all-reduce per optimizer step -> identical parameters on both ranks after the update."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (a, b, n) for r, a, b, n in (q.get(timeout=240) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+    assert all(b is not None for _, b, _ in res.values()), res
+    (a0, b0, n0), (a1, b1, n1) = res[0], res[1]
+    assert n0 == n1 == 4
+    assert np.array_equal(a0, a1)                  # same init
+    assert np.abs(b0 - a0).max() > 1e-5            # the update moved the policy
+    np.testing.assert_array_equal(b0, b1)          # ... identically on both ranks
