@@ -317,6 +317,86 @@ def _cpu_baseline(seconds: float) -> dict:
                       f"1 thread, {dt:.1f} s on {platform.processor() or platform.machine()}"}
 
 
+def _cpu_baseline_ppo(seconds: float) -> dict:
+    """SURVEY config 1 on the host: the reference's CPU training loop shape -- train.py's 16 envs
+    (HoverEnv + RateControlWrapper) stepped one after another (DummyVecEnv) through the float64 C
+    oracle, a torch-CPU ActorCritic with SB3 semantics, GAE, and the SB3 update (n_epochs x
+    minibatches of 128 rows, clip_grad_norm_, Adam), 1 torch thread. Bounded: one rollout of
+    n_steps and as many update minibatches as fit the time budget, extrapolated per iteration."""
+    import numpy as np
+    from oracle import oracle as O
+    from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig, ppo_loss
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        cfg = PPOConfig()
+        n_envs, T = 16, cfg.n_steps
+        ocfg = O.default_cfg(O.ENV_HOVER, O.WRAP_CTBR)
+        envs = [O.Env(cfg=ocfg) for _ in range(n_envs)]
+        episode = [0] * n_envs
+        obs = np.stack([e.reset_with(*O.reset_draw(ocfg, 0, i, 0)) for i, e in enumerate(envs)])
+        torch.manual_seed(0)
+        pol = ActorCritic()
+        opt = torch.optim.Adam(pol.parameters(), lr=cfg.learning_rate, eps=cfg.adam_eps)
+        buf = {k: torch.zeros(T, n_envs, d) for k, d in (("obs", 12), ("act", 4))}
+        lp_b, v_b, r_b, s_b = (torch.zeros(T, n_envs) for _ in range(4))
+        start = torch.ones(n_envs)
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            for t in range(T):
+                o = torch.from_numpy(obs)
+                mean, v = pol.forward_heads(o)
+                a = mean + pol.log_std.exp() * torch.randn_like(mean)
+                buf["obs"][t], buf["act"][t], lp_b[t], v_b[t], s_b[t] = o, a, pol.log_prob(mean, a), v, start
+                ac = a.clamp(-1, 1).numpy()
+                for i, e in enumerate(envs):
+                    out = e.step(ac[i])
+                    r = float(out.reward)
+                    if out.truncated and not out.terminated:  # TimeLimit bootstrap
+                        r += cfg.gamma * float(pol.value(torch.from_numpy(np.array(out.obs[:], np.float32))[None])[0])
+                    r_b[t, i] = r
+                    done = bool(out.terminated or out.truncated)
+                    start[i] = float(done)
+                    if done:
+                        episode[i] += 1
+                        obs[i] = e.reset_with(*O.reset_draw(ocfg, 0, i, episode[i]))
+                    else:
+                        obs[i] = np.array(out.obs[:], np.float32)
+            last_v = pol.value(torch.from_numpy(obs))
+        adv, ret = torch.zeros(T, n_envs), torch.zeros(T, n_envs)
+        gae_acc = torch.zeros(n_envs)
+        for t in reversed(range(T)):  # SB3 RolloutBuffer.compute_returns_and_advantage
+            nv, nnt = (last_v, 1.0 - start) if t == T - 1 else (v_b[t + 1], 1.0 - s_b[t + 1])
+            delta = r_b[t] + cfg.gamma * nv * nnt - v_b[t]
+            gae_acc = delta + cfg.gamma * cfg.gae_lambda * nnt * gae_acc
+            adv[t] = gae_acc
+        ret = adv + v_b
+        t_roll = time.perf_counter() - t0
+        M, B = T * n_envs, 128
+        flat = [buf["obs"].view(M, 12), buf["act"].view(M, 4), lp_b.view(M), adv.view(M), ret.view(M)]
+        steps_total = cfg.n_epochs * (M // B)
+        t1, done = time.perf_counter(), 0
+        budget = max(1.0, seconds - t_roll)
+        while done < steps_total and time.perf_counter() - t1 < budget:
+            idx = torch.randperm(M)[:B]
+            loss = ppo_loss(pol, *[x[idx] for x in flat], cfg)[0]
+            opt.zero_grad()
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(pol.parameters(), cfg.max_grad_norm)
+            opt.step()
+            done += 1
+        t_upd = (time.perf_counter() - t1) * steps_total / max(done, 1)
+        it = t_roll + t_upd
+        return {"value": M / it, "unit": "env-steps/s (whole PPO iteration)", "cores": 1, "kind": "port",
+                "sample": f"train.py loop on the host: 16 oracle envs (HoverEnv + RateControlWrapper, DummyVecEnv "
+                          f"order) x {T} steps + torch-CPU PPO update (SB3 schedule: {steps_total} Adam steps of "
+                          f"{B} rows; {done} timed, extrapolated), 1 thread; rollout {t_roll:.1f} s, update "
+                          f"{t_upd:.1f} s per iteration"}
+    finally:
+        torch.set_num_threads(threads)
+
+
 def _pmc_traffic(n_envs: int):
     """HBM bytes per quad_step launch from the committed rocprofv3 PMC summary, if present."""
     path = os.path.join(REPO, "profiles", "pmc_quad_step.json")
@@ -405,6 +485,7 @@ def main():
                                "achieved_GBs": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9}
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = _cpu_baseline(args.cpu_seconds)
+        line["cpu_baseline_ppo"] = _cpu_baseline_ppo(args.cpu_seconds)
     print(json.dumps(line), flush=True)
 
 
