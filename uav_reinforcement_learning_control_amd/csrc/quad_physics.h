@@ -127,9 +127,12 @@ QD_HD float div_const(float a, float b, float rb) {
 }
 
 // np.clip semantics: NaN propagates
+// (two flat selects: NaN fails both compares and passes through; lo <= hi. The nested form with an
+// explicit NaN test compiled to divergent branches -- 20 exec-mask regions per k_step.)
 template <typename T>
 QD_HD T clipn(T x, T lo, T hi) {
-  return (x != x) ? x : (x < lo ? lo : (x > hi ? hi : x));
+  const T a = x < lo ? lo : x;
+  return a > hi ? hi : a;
 }
 // mju_isBad: NaN or |x| > 1e10 (one compare with an abs modifier)
 template <typename T>
