@@ -117,13 +117,13 @@ QD_HD float q_atan2(float y, float x) {
 
 // a / b for a constant b with precomputed rb = RN(1/b): Markstein's correction returns the
 // correctly rounded quotient; verified exhaustively over all 2^32 float32 a for the five
-// observation spans (every mismatch is a subnormal quotient or -0, neither reachable here;
-// -0 is handled by the select).
+// observation spans (every mismatch is a subnormal quotient, unreachable here, or the sign of a
+// zero quotient: -0 comes back +0, which its only caller -- norm_obs1, v - 1 -- cannot see).
 QD_HD float div_const(float a, float b, float rb) {
 #pragma clang fp contract(off)
   const float q = a * rb;
   const float e = fmaf(-q, b, a);
-  return e == 0.0f ? q : fmaf(e, rb, q);
+  return fmaf(e, rb, q);
 }
 
 // np.clip semantics: NaN propagates
@@ -413,7 +413,7 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double f = badctrl ? 0.0 : Fin[i];
-    F[i] = f < c.ctrl_lo ? c.ctrl_lo : (f > c.ctrl_hi ? c.ctrl_hi : f);
+    F[i] = clipn(f, c.ctrl_lo, c.ctrl_hi);  // (flat selects; f is never NaN here)
   }
   T Fsum = T(F[0] + F[1] + F[2] + F[3]);
   T taum[3] = {T(c.syd[0] * F[0] + c.syd[1] * F[1] + c.syd[2] * F[2] + c.syd[3] * F[3]),
