@@ -139,3 +139,13 @@ def test_split_k_linear_gradients_match_plain():
     assert torch.equal(y, y2) and torch.allclose(gx, gx2, atol=1e-5)
     assert torch.allclose(gw, gw2, rtol=1e-4, atol=1e-3) and torch.allclose(gb, gb2, rtol=1e-4, atol=1e-3)
     assert P._chunks(100_000) == 16 and P._chunks(3) == 1
+
+
+def test_cpu_ppo_baseline_runs_the_reference_loop_shape():
+    """bench.py's cpu_baseline_ppo (SURVEY config 1): 16 oracle envs + CTBR through a full rollout,
+    GAE and a (time-bounded, extrapolated) SB3 update on the host, one thread."""
+    import bench
+    r = bench._cpu_baseline_ppo(2.0)
+    assert r["cores"] == 1 and r["kind"] == "port" and r["value"] > 0
+    assert "16 oracle envs" in r["sample"] and "2560 Adam steps" in r["sample"]
+    assert torch.get_num_threads() >= 1  # the thread count is restored
