@@ -487,18 +487,16 @@ QD_HD void quat_to_euler(const T qin[4], T e[3]) {
   T mid = T(2) * q_atan2(q_hypot(c, d), q_hypot(a, b));
   const bool case1 = q_abs(mid) <= T(1e-7), case2 = q_abs(mid - PI) <= T(1e-7);
   const T hs = q_atan2(b, a), hd = q_atan2(d, c);
-  if (!(case1 || case2)) {
-    e[0] = hs - hd;
-    e[2] = hs + hd;
-  } else {
-    e[2] = T(0);
-    e[0] = case1 ? T(2) * hs : T(-2) * hd;
-  }
+  // (selects, not branches: the if/else forms compiled to seven exec-mask regions per step)
+  const bool gimbal = case1 || case2;
+  const T e0g = case1 ? T(2) * hs : T(-2) * hd;
+  e[0] = gimbal ? e0g : hs - hd;
+  e[2] = gimbal ? T(0) : hs + hd;
   e[1] = mid - PI / T(2);
 #pragma unroll
   for (int i = 0; i < 3; i++) {
-    if (e[i] < -PI) e[i] += T(2) * PI;
-    else if (e[i] > PI) e[i] -= T(2) * PI;
+    const T up = e[i] + T(2) * PI, dn = e[i] - T(2) * PI;
+    e[i] = e[i] < -PI ? up : (e[i] > PI ? dn : e[i]);
   }
 }
 
