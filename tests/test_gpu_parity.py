@@ -236,6 +236,41 @@ def test_nan_and_extreme_actions(kernel_variant):
     env.close()
 
 
+def test_bad_state_and_acceleration_resets(kernel_variant):
+    """MuJoCo's mj_checkPos/Vel (NaN/Inf or |x| > 1e10 in qpos/qvel -> mj_resetData) and
+    mj_checkAcc, and large-but-good states whose |x| sum exceeds 1e10 (the kernel's screen then
+    falls back to per-element tests, which must find nothing bad)."""
+    n = 512
+    rng = np.random.default_rng(11)
+    st = _random_states(n, rng, wide=False)
+    st["step_count"][:] = 0
+    k = np.arange(n) % 8
+    st["qpos"][k == 0, 0] = np.nan
+    st["qvel"][k == 1, 1] = 2e10
+    st["qpos"][k == 2, 4] = np.inf
+    st["qvel"][k == 3, 3:5] = 6e9      # good state, sum > 1e10; angular rate -> bad acceleration
+    st["qvel"][k == 4, 6:8] = 6e9      # prop spins: good state, bad acceleration
+    st["qvel"][k == 5, 0:2] = 6e9      # linear velocity: good state, bad acceleration (drag)
+    st["qpos"][k == 6, 3:5] = 6e9      # unnormalized quaternion: good state, normalized by the step
+    acts = rng.uniform(-1, 1, (n, 4)).astype(np.float32)
+    env = _env(n, auto_reset=False)
+    g = _gpu_step(env, st, acts)
+    ref = _oracle_step(O.ENV_HOVER, O.WRAP_NONE, st, acts)
+    for i, o in enumerate(ref):
+        assert g["terminated"][i] == o["terminated"], i
+        # pre-step scale without the NaN / huge entries (they would void or loosen the check)
+        pp, pv = (np.where(np.abs(st[f][i]) < 1e9, st[f][i], 0) for f in ("qpos", "qvel"))
+        assert parity_ok(g["qpos"][i], o["qpos"], pp), (i, g["qpos"][i], o["qpos"])
+        assert parity_ok(g["qvel"][i], o["qvel"], pv), (i, g["qvel"][i], o["qvel"])
+        assert parity_ok(g["obs"][i], o["obs"]), i
+    # bad states (rows 0-2) and bad accelerations (rows 3-5) really were reset to qpos0: unit
+    # quaternion, zero hinge angles, zero angular and prop rates (only gravity acts afterwards)
+    for i in np.nonzero(k <= 5)[0]:
+        assert np.array_equal(g["qvel"][i][3:], np.zeros(7, np.float32)), i
+        assert np.array_equal(g["qpos"][i][3:], np.array([1, 0, 0, 0, 0, 0, 0, 0], np.float32)), i
+    env.close()
+
+
 def test_large_batch_properties():
     """Full-size batch (1,048,576 envs): size-independent properties + a strided oracle sample."""
     n = 1 << 20

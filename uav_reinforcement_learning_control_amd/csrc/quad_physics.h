@@ -139,6 +139,27 @@ template <typename T>
 QD_HD bool isbad(T x) {
   return !(q_abs(x) <= T(1e10));
 }
+// any(mju_isBad(x_i)). A rounded sum of non-negative terms is >= each term and NaN if any term
+// is, so sum |x_i| <= 1e10 proves no x_i is bad; the per-element tests run only when that screen
+// fails. (Per element, each test is a compare plus a scalar mask OR: 2 issue slots vs 1 add.)
+// On the device the screen is wave-uniform (a ballot), so the exact tests sit behind a scalar
+// branch the compiler cannot if-convert back into the straight-line path.
+template <typename T, int N>
+QD_HD bool any_bad(const T (&x)[N]) {
+  T acc[4] = {q_abs(x[0]), T(0), T(0), T(0)};
+#pragma unroll
+  for (int i = 1; i < N; i++) acc[i & 3] += q_abs(x[i]);
+  const bool ok = (acc[0] + acc[1]) + (acc[2] + acc[3]) <= T(1e10);
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (__builtin_amdgcn_ballot_w64(!ok) == 0) return false;
+#else
+  if (ok) return false;
+#endif
+  bool b = false;
+#pragma unroll
+  for (int i = 0; i < N; i++) b |= isbad(x[i]);
+  return b;
+}
 
 // ---------------------------------------------------------------------------------------------
 template <typename T>
@@ -391,11 +412,9 @@ QD_HD void normalize4(T q[4]) {
 template <typename T, bool CHECKS = true>
 QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4]) {
   // mj_checkPos / mj_checkVel: bad state => mj_resetData (qpos0, zero qvel, zero ctrl)
-  bool bad = false;
-#pragma unroll
-  for (int i = 0; i < 3; i++) bad |= int(isbad(e.pos[i])) | int(isbad(e.v[i])) | int(isbad(e.w[i]));
-#pragma unroll
-  for (int i = 0; i < 4; i++) bad |= int(isbad(e.q[i])) | int(isbad(e.th[i])) | int(isbad(e.s[i]));
+  const T st[21] = {e.pos[0], e.pos[1], e.pos[2], e.q[0], e.q[1], e.q[2], e.q[3], e.th[0], e.th[1], e.th[2], e.th[3],
+                    e.v[0], e.v[1], e.v[2], e.w[0], e.w[1], e.w[2], e.s[0], e.s[1], e.s[2], e.s[3]};
+  bool bad = any_bad(st);
   bool badctrl = false;
 #pragma unroll
   for (int i = 0; i < 4; i++) badctrl |= isbad(Fin[i]);
@@ -423,11 +442,8 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
   normalize4(qn);
   T vdot[3], wdot[3], sdot[4];
   forward_acc(c, qn, e.th, e.v, e.w, e.s, Fsum, taum, vdot, wdot, sdot);
-  bool badacc = false;
-#pragma unroll
-  for (int i = 0; i < 3; i++) badacc |= int(isbad(vdot[i])) | int(isbad(wdot[i]));
-#pragma unroll
-  for (int i = 0; i < 4; i++) badacc |= isbad(sdot[i]);
+  const T acc[10] = {vdot[0], vdot[1], vdot[2], wdot[0], wdot[1], wdot[2], sdot[0], sdot[1], sdot[2], sdot[3]};
+  const bool badacc = any_bad(acc);
   if (CHECKS && badacc) {  // mj_checkAcc: reset to qpos0 with zero ctrl; at rest there the only force is
                  // gravity, so qacc = (0, 0, gz, 0, ...) exactly (cf. oracle K1)
 #pragma unroll
