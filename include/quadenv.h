@@ -60,7 +60,7 @@ typedef struct QuadCfg {
   float target_low[3], target_high[3];   /* HoverEnv._target_pos_bounds (hover only) */
   float term_low[12], term_high[12];     /* HoverEnv._state_bounds (termination) */
   float act_low[4], act_high[4];         /* HoverEnv._action_bounds */
-  double max_motor_thrust, arm_length, yaw_coeff;
+  double max_motor_thrust, arm_length, yaw_coeff; /* max_motor_thrust: finite, >= 0 (else QUAD_EINVAL) */
   double nominal_voltage, min_voltage, vdrop_base, vdrop_load;
   double rate_max_rad, rate_kd[3], rate_ki, rate_imax, inertia[3], max_torque;
   double timestep, gravity[3], density, viscosity;

@@ -627,7 +627,11 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
   }
   const double vs = clipn(double(e.volt) * k.r_vnom, 0.0, 1.0);
 #pragma unroll
-  for (int i = 0; i < 4; i++) F[i] = clipn(F[i] * vs, 0.0, k.max_thrust * vs);
+  // hover_env.py:175 clips F * vs to [0, max_thrust * vs]; that clip never binds here: F is in
+  // [0, max_thrust] (or NaN) after the clip above, vs in [0, 1] (or NaN), max_thrust >= 0 (checked
+  // by quad_create), and a rounded product with the same non-negative vs is monotone in F
+  // (F * vs <= max_thrust * vs); NaN passes either way.
+  for (int i = 0; i < 4; i++) F[i] = F[i] * vs;
   const double load = ((F[0] + F[1] + F[2] + F[3]) * 0.25) * k.r_mx;
   const double dV = (k.vb + k.vl * load) * k.dt;
   e.volt = T(clipn(double(e.volt) - dV, k.vmin, k.vnom));

@@ -1115,6 +1115,8 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   if (cfg->env_kind >= QUAD_ENV_BRAX_HOVER && cfg->wrapper != QUAD_WRAP_NONE)
     return fail(QUAD_EINVAL, "the brax env kinds take no wrapper");
   if (cfg->max_episode_steps <= 0) return fail(QUAD_EINVAL, "max_episode_steps must be > 0");
+  if (!(cfg->max_motor_thrust >= 0.0 && cfg->max_motor_thrust <= 1e30))
+    return fail(QUAD_EINVAL, "max_motor_thrust must be finite and >= 0");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(QUAD_EINVAL, "device out of range");
