@@ -698,12 +698,20 @@ QD_HD void reset_block(uint64_t seed, uint64_t gid, uint32_t episode, uint32_t b
   c[0] = uint32_t(gid); c[1] = uint32_t(gid >> 32); c[2] = episode; c[3] = blk;
   philox4x32_10(c, uint32_t(seed), uint32_t(seed >> 32));
 }
+// (from the uniforms u = u01(word); the wave-compacted kernels convert where the words are made)
+QD_HD void reset_affine_u(const float init_lo[12], const float init_span[12], const float tgt_lo[3],
+                          const float tgt_span[3], const float u[16], float init12[12], float tgt[3]) {
+#pragma unroll
+  for (int i = 0; i < 12; i++) init12[i] = affine32(init_lo[i], u[i], init_span[i]);
+#pragma unroll
+  for (int i = 0; i < 3; i++) tgt[i] = affine32(tgt_lo[i], u[12 + i], tgt_span[i]);
+}
 QD_HD void reset_affine(const float init_lo[12], const float init_span[12], const float tgt_lo[3],
                         const float tgt_span[3], const uint32_t r[16], float init12[12], float tgt[3]) {
+  float u[16];
 #pragma unroll
-  for (int i = 0; i < 12; i++) init12[i] = affine32(init_lo[i], u01(r[i]), init_span[i]);
-#pragma unroll
-  for (int i = 0; i < 3; i++) tgt[i] = affine32(tgt_lo[i], u01(r[12 + i]), tgt_span[i]);
+  for (int i = 0; i < 16; i++) u[i] = u01(r[i]);
+  reset_affine_u(init_lo, init_span, tgt_lo, tgt_span, u, init12, tgt);
 }
 QD_HD void reset_draw(const float init_lo[12], const float init_span[12], const float tgt_lo[3],
                       const float tgt_span[3], uint64_t seed, uint64_t gid, uint32_t episode,

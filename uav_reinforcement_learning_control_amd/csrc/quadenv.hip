@@ -78,13 +78,15 @@ __device__ __forceinline__ void reset_env(const KParams& p, int i, EnvRegs<float
 // item, and the resetting lanes read back their 16 words. With <= 16 resets per wave (the common
 // case) that is one Philox pass for the wave instead of four serial ones per resetting lane: a
 // Philox block is 20 quarter-rate v_mad_u64_u32, and the draw was half the reset branch.
-// Identical words to reset_draw (same counters). Called by every active lane of the wave.
+// Identical words to reset_draw (same counters), handed back as the uniforms u01(word): converted
+// by the lane that made the block, 4 per lane instead of 16 in each resetting lane's stream.
+// Called by every active lane of the wave.
 struct ResetLds {
   uint32_t env[4][64], ep[4][64];
-  uint4 words[4][256];  // [wave][rank * 4 + block]
+  float4 words[4][256];  // [wave][rank * 4 + block]
 };
 __device__ __forceinline__ void reset_words_wave(const KParams& p, ResetLds& L, uint32_t i, uint32_t ep,
-                                                 bool rs, uint32_t r16[16]) {
+                                                 bool rs, float u16[16]) {
   const uint64_t m = __ballot(rs);
   if (m == 0) return;
   const int w = threadIdx.x >> 6, lane = __lane_id();
@@ -98,15 +100,15 @@ __device__ __forceinline__ void reset_words_wave(const KParams& p, ResetLds& L, 
     if (rr < nres) {
       uint32_t c[4];
       reset_block(p.seed, p.gid_base + uint64_t(L.env[w][rr]), L.ep[w][rr], uint32_t(item & 3), c);
-      L.words[w][item] = make_uint4(c[0], c[1], c[2], c[3]);
+      L.words[w][item] = make_float4(u01(c[0]), u01(c[1]), u01(c[2]), u01(c[3]));
     }
   }
   __builtin_amdgcn_wave_barrier();
   if (rs) {
 #pragma unroll
     for (int b = 0; b < 4; b++) {
-      const uint4 v = L.words[w][rank * 4 + b];
-      r16[4 * b] = v.x; r16[4 * b + 1] = v.y; r16[4 * b + 2] = v.z; r16[4 * b + 3] = v.w;
+      const float4 v = L.words[w][rank * 4 + b];
+      u16[4 * b] = v.x; u16[4 * b + 1] = v.y; u16[4 * b + 2] = v.z; u16[4 * b + 3] = v.w;
     }
   }
 }
@@ -208,12 +210,12 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
 #else
     const bool rs = live && (r.term || r.trunc) && p.auto_reset;
 #endif
-    uint32_t r16[16];
-    reset_words_wave(p, rl, uint32_t(i), ep, rs, r16);
+    float u16[16];
+    reset_words_wave(p, rl, uint32_t(i), ep, rs, u16);
     if (rs) {
       if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
       float init12[12], tgt[3], s12[12];
-      reset_affine(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, r16, init12, tgt);
+      reset_affine_u(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, u16, init12, tgt);
       env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
       S.stu(F_EP, vo, ep + 1u);
     }

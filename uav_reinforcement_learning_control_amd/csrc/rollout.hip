@@ -64,7 +64,7 @@ __device__ __forceinline__ void fragments(const float ob[12], float (&xb)[NT][6]
 template <int KEY_MASK>
 __device__ __forceinline__ void reset_words_shfl(const KParams& p, uint32_t (&renv)[64], uint32_t (&rep)[64],
                                                  uint32_t i, uint32_t ep, bool publish, bool apply,
-                                                 uint32_t r16[16]) {
+                                                 float u16[16]) {
   const uint64_t m = __ballot(publish);
   if (m == 0) return;
   const int lane = __lane_id();
@@ -77,14 +77,17 @@ __device__ __forceinline__ void reset_words_shfl(const KParams& p, uint32_t (&re
     const int item = t * 64 + lane, rr = item >> 2;
     uint32_t c[4] = {0u, 0u, 0u, 0u};
     if (rr < nres) reset_block(p.seed, p.gid_base + uint64_t(renv[rr]), rep[rr], uint32_t(item & 3), c);
+    float cu[4];  // the uniforms u01(word), converted here: 4 per lane instead of 16 per resetting lane
+#pragma unroll
+    for (int k = 0; k < 4; k++) cu[k] = u01(c[k]);
     const bool mine = apply && (rank >> 4) == t;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
       const int src = (rank * 4 + b) & 63;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        const uint32_t v = uint32_t(__shfl(int(c[k]), src));
-        if (mine) r16[4 * b + k] = v;
+        const float v = __shfl(cu[k], src);
+        if (mine) u16[4 * b + k] = v;
       }
     }
   }
@@ -213,11 +216,11 @@ __global__ __launch_bounds__(512 / NT) void k_rollout(const KConsts<float>* __re
     for (int j = 0; j < 12; j++) ob[j] = r.obs[j];
     // ---- SB3 auto-reset: the next step starts from the reset observation
     const bool rs = ok && done;
-    uint32_t r16[16];
-    reset_words_shfl<NT == 2 ? 63 : 31>(p, renv[w], rep[w], uint32_t(i), ep, owner && done, rs, r16);
+    float u16[16];
+    reset_words_shfl<NT == 2 ? 63 : 31>(p, renv[w], rep[w], uint32_t(i), ep, owner && done, rs, u16);
     if (rs) {
       float init12[12], tgt[3], s12[12];
-      reset_affine(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, r16, init12, tgt);
+      reset_affine_u(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, u16, init12, tgt);
       env_reset_from<float, KIND>(*p.kc, e, init12, tgt, ob, s12);
       ep += 1u;
     }
