@@ -67,6 +67,8 @@ QD_HD float q_rsqrt(float x) { return frsqrt(x); }
 QD_HD double q_atan2(double y, double x) { return atan2(y, x); }
 QD_HD double q_hypot(double x, double y) { return hypot(x, y); }
 QD_HD float q_hypot(float x, float y) { return fsqrt(x * x + y * y); }  // |args| <= 2 here
+QD_HD float q_fma(float a, float b, float c) { return fmaf(a, b, c); }
+QD_HD double q_fma(double a, double b, double c) { return fma(a, b, c); }
 QD_HD float q_abs(float x) { return fabsf(x); }
 QD_HD double q_abs(double x) { return fabs(x); }
 QD_HD float q_exp(float x) { return expf(x); }
@@ -298,9 +300,9 @@ template <typename T>
 QD_HD void box_drag(const T w[3], const T u[3], const T kqa[3], const T kva, const T kql[3],
                     const T kvl, T t[3], T f[3]) {
 #pragma unroll
-  for (int j = 0; j < 3; j++) {
-    t[j] = -kva * w[j] - kqa[j] * q_abs(w[j]) * w[j];
-    f[j] = -kvl * u[j] - kql[j] * q_abs(u[j]) * u[j];
+  for (int j = 0; j < 3; j++) {  // -(kv + kq |x|) x: an fma and a multiply per component
+    t[j] = -(kva + kqa[j] * q_abs(w[j])) * w[j];
+    f[j] = -(kvl + kql[j] * q_abs(u[j])) * u[j];
   }
 }
 
@@ -341,24 +343,27 @@ QD_HD void forward_acc(const PhysConsts<T>& c, const T qn[4], const T th[4], con
     for (int i = 0; i < 3; i++) { FB[i] += f[i]; tau[i] += t[i]; }
   }
   // prop fluid: prop frame = base frame rotated by th_i about z; COM on the axis at pc_i
+  // (written as explicit fma chains: -ffp-contract=on fuses only within one expression, and the
+  // cross products, frame rotations and accumulations below are ~1/3 of the physics)
   T Qs[4];
 #pragma unroll
   for (int p = 0; p < 4; p++) {
     T sn, cs;
     q_sincos(th[p], &sn, &cs);
-    T wxc[3];
-    cross(w, c.pc[p], wxc);
-    const T ub[3] = {vB[0] + wxc[0], vB[1] + wxc[1], vB[2] + wxc[2]};
-    const T wp[3] = {cs * w[0] + sn * w[1], -sn * w[0] + cs * w[1], w[2] + s[p]};
-    const T up[3] = {cs * ub[0] + sn * ub[1], -sn * ub[0] + cs * ub[1], ub[2]};
+    const T* r = c.pc[p];
+    const T ub[3] = {q_fma(w[1], r[2], q_fma(-w[2], r[1], vB[0])),  // vB + w x r
+                     q_fma(w[2], r[0], q_fma(-w[0], r[2], vB[1])),
+                     q_fma(w[0], r[1], q_fma(-w[1], r[0], vB[2]))};
+    const T wp[3] = {q_fma(cs, w[0], sn * w[1]), q_fma(-sn, w[0], cs * w[1]), w[2] + s[p]};
+    const T up[3] = {q_fma(cs, ub[0], sn * ub[1]), q_fma(-sn, ub[0], cs * ub[1]), ub[2]};
     T tp[3], fp[3];
     box_drag(wp, up, c.p_kqa, c.p_kva, c.p_kql, c.p_kvl, tp, fp);
-    const T f[3] = {cs * fp[0] - sn * fp[1], sn * fp[0] + cs * fp[1], fp[2]};
-    const T t[3] = {cs * tp[0] - sn * tp[1], sn * tp[0] + cs * tp[1], tp[2]};
-    T rxf[3];
-    cross(c.pc[p], f, rxf);
-#pragma unroll
-    for (int i = 0; i < 3; i++) { FB[i] += f[i]; tau[i] += rxf[i] + t[i]; }
+    const T f[3] = {q_fma(cs, fp[0], -sn * fp[1]), q_fma(sn, fp[0], cs * fp[1]), fp[2]};  // back to base
+    FB[0] += f[0]; FB[1] += f[1]; FB[2] += f[2];
+    // tau += r x f + Rz(th) tp
+    tau[0] = q_fma(r[1], f[2], q_fma(-r[2], f[1], q_fma(cs, tp[0], q_fma(-sn, tp[1], tau[0]))));
+    tau[1] = q_fma(r[2], f[0], q_fma(-r[0], f[2], q_fma(sn, tp[0], q_fma(cs, tp[1], tau[1]))));
+    tau[2] = q_fma(r[0], f[1], q_fma(-r[1], f[0], tau[2] + tp[2]));
     Qs[p] = tp[2];
   }
   // velocity-product (bias) terms
