@@ -95,6 +95,22 @@ QD_HD void q_sincos(float x, float* s, float* c) {
   *c = ((qi + 1) & 2) ? -b : b;
 }
 
+// sin/cos of a prop hinge angle, which only orients that prop's drag box: on the device the
+// hardware v_sin_f32 / v_cos_f32 on the angle in revolutions, reduced to [-1/2, 1/2] (error ~1e-6
+// rad plus the reduction's ulp(|x| / 2pi); the float32 angle itself carries ulp(|x|)). ~5 issue
+// slots instead of ~22 for q_sincos. The host instantiation keeps libm.
+QD_HD void prop_sincos(float x, float* s, float* c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  float r = x * 0.159154943091895336f;
+  r -= rintf(r);
+  *s = __builtin_amdgcn_sinf(r);
+  *c = __builtin_amdgcn_cosf(r);
+#else
+  q_sincos(x, s, c);
+#endif
+}
+QD_HD void prop_sincos(double x, double* s, double* c) { q_sincos(x, s, c); }
+
 // atan2: odd degree-17 polynomial for atan on [0, 1] (float32 evaluation error 1.1e-7),
 // octant fix-ups. Matches atan2's conventions for signed zeros and the axes.
 QD_HD float q_atan2(float y, float x) {
@@ -349,7 +365,7 @@ QD_HD void forward_acc(const PhysConsts<T>& c, const T qn[4], const T th[4], con
 #pragma unroll
   for (int p = 0; p < 4; p++) {
     T sn, cs;
-    q_sincos(th[p], &sn, &cs);
+    prop_sincos(th[p], &sn, &cs);
     const T* r = c.pc[p];
     const T ub[3] = {q_fma(w[1], r[2], q_fma(-w[2], r[1], vB[0])),  // vB + w x r
                      q_fma(w[2], r[0], q_fma(-w[0], r[2], vB[1])),
