@@ -34,7 +34,8 @@ struct ModelData {
   double Ip[3] = {3.75335e-06, 1.87898e-06, 1.87898e-06};
   // motors on sites thrust1..4 == prop positions (drone.xml:73-76, 81-84)
   double gear5[4] = {0.0201, -0.0201, 0.0201, -0.0201};
-  double ctrl_lo = 0.0, ctrl_hi = 13.0;  // ctrlrange (drone.xml:9), autolimits (:2)
+  double ctrl_lo = 0.0, ctrl_hi = 13.0;  // ctrlrange (drone.xml:9), autolimits (:2); ctrl_lo <= 0 is
+                                         // assumed by physics_step<.., F_NONNEG = true>
 };
 
 // Everything the kernel needs, in double; cast to float for the device.

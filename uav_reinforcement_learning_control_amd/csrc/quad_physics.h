@@ -430,7 +430,9 @@ QD_HD void normalize4(T q[4]) {
 // mujoco.mj_step for one env. Fin: ctrl in float64 (may be NaN / out of range; MuJoCo semantics).
 // CHECKS = false: mjx.step semantics (the brax kinds): no bad-state / bad-ctrl / bad-acc resets,
 // NaN propagates.
-template <typename T, bool CHECKS = true>
+// F_NONNEG: the caller guarantees Fin >= 0 (or -0, or NaN) -- env_step's F * vs -- so the
+// ctrlrange clamp's lower bound (drone.xml's fixed 0, quad_model.h) cannot bind and is skipped.
+template <typename T, bool CHECKS = true, bool F_NONNEG = false>
 QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4]) {
   // mj_checkPos / mj_checkVel: bad state => mj_resetData (qpos0, zero qvel, zero ctrl)
   const T st[21] = {e.pos[0], e.pos[1], e.pos[2], e.q[0], e.q[1], e.q[2], e.q[3], e.th[0], e.th[1], e.th[2], e.th[3],
@@ -453,7 +455,10 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double f = badctrl ? 0.0 : Fin[i];
-    F[i] = clipn(f, c.ctrl_lo, c.ctrl_hi);  // (flat selects; f is never NaN here)
+    if (F_NONNEG)  // ctrl_lo <= 0 <= f: only the upper bound can bind
+      F[i] = f > c.ctrl_hi ? c.ctrl_hi : f;
+    else
+      F[i] = clipn(f, c.ctrl_lo, c.ctrl_hi);  // (flat selects; f is never NaN here)
   }
   T Fsum = T(F[0] + F[1] + F[2] + F[3]);
   T taum[3] = {T(c.syd[0] * F[0] + c.syd[1] * F[1] + c.syd[2] * F[2] + c.syd[3] * F[3]),
@@ -667,10 +672,10 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
   e.volt = T(clipn(double(e.volt) - dV, k.vmin, k.vnom));
   // QD_ABL_*: cost-ablation builds of tools/step_variants.py only (never defined in the product)
 #if defined(QD_ABL_PHYS2)
-  physics_step(k.ph, e, F);
-  physics_step(k.ph, e, F);
+  physics_step<T, true, true>(k.ph, e, F);
+  physics_step<T, true, true>(k.ph, e, F);
 #elif !defined(QD_ABL_NOPHYS)
-  physics_step(k.ph, e, F);
+  physics_step<T, true, true>(k.ph, e, F);  // F = clip(., 0, max) * vs >= 0 (or NaN)
 #endif
   e.step += 1;
 #if defined(QD_ABL_NOOBS)
