@@ -51,19 +51,46 @@ def _quad_step_fn(env):
     return step
 
 
-def _kernel_time_us(env, step, actions, n_launch: int) -> float:
-    """Average device duration of one quad_step launch: HIP event pair around each launch on
-    the stream the kernel runs on (torch's current stream)."""
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(n_launch)]
+def _graph_of(step, actions, first: int, n: int):
+    """Capture n step launches (action batches first.. in order) into one hipGraph and upload its
+    executable, so that its first replay does not pay instantiation/upload costs."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for k in range(n):
+            step(actions[(first + k) % len(actions)].data_ptr())
+    _graph_upload(g)
+    return g
+
+
+def _graph_upload(g) -> None:
+    """hipGraphUpload of a captured torch graph's executable on the current stream (torch already
+    loaded the HIP runtime, so dlopen by soname returns that same library)."""
+    try:
+        hip = C.CDLL("libamdhip64.so.7")
+        rc = hip.hipGraphUpload(C.c_void_p(g.raw_cuda_graph_exec()),
+                                C.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"hipGraphUpload returned {rc}")
+    except (AttributeError, OSError):
+        pass  # older torch without raw_cuda_graph_exec: the untimed warm replay below covers it
+
+
+def _gated_kernel_us(step, actions, n_launch: int = 200) -> float:
+    """Average device time per launch of back-to-back graph-replayed step launches, HIP events on
+    the launching stream. A short spin kernel ahead of the first event keeps the GPU busy while
+    the host submits, so the interval holds only the launches (the roofline's kernel time)."""
+    chunk = 100
+    g = _graph_of(step, actions, 0, chunk)
+    g.replay()
     torch.cuda.synchronize()
-    for k in range(n_launch):
-        ev[k][0].record()
-        step(actions[k % len(actions)].data_ptr())
-        ev[k][1].record()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(200_000)  # ~100 us gate
+    e0.record()
+    for _ in range(max(1, n_launch // chunk)):
+        g.replay()
+    e1.record()
     torch.cuda.synchronize()
-    ts = sorted(a.elapsed_time(b) * 1e3 for a, b in ev)
-    return sum(ts[: max(1, int(0.9 * len(ts)))]) / max(1, int(0.9 * len(ts)))  # drop top 10 %
+    return e0.elapsed_time(e1) * 1e3 / (max(1, n_launch // chunk) * chunk)
 
 
 def _run_rank(args, rank, world, local_rank):
@@ -79,18 +106,16 @@ def _run_rank(args, rank, world, local_rank):
     step = _quad_step_fn(env)
     chunk = args.graph_chunk if args.steps % args.graph_chunk == 0 else args.steps
 
-    # warmup (eager), then capture the step sequence into a hipGraph
-    for k in range(args.warmup):
-        step(actions[k % n_act].data_ptr())
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for k in range(chunk):
-            step(actions[(args.warmup + k) % n_act].data_ptr())
+    # the timed step sequence as hipGraph(s), captured and uploaded before the warmup; the W
+    # warmup steps are replays of a graph of the same launches (first kernel runs, caches, TLB)
+    g = _graph_of(step, actions, args.warmup, chunk)
+    if args.warmup > 0:
+        gw = _graph_of(step, actions, 0, args.warmup)
+        gw.replay()
     torch.cuda.synchronize()
 
-    # timed region: exactly K steps; HIP events on the stream the kernels run on give the
-    # average launch duration (graph replay leaves no host gap between launches)
+    # timed region: exactly K steps, barrier + synchronize on both sides; HIP events on the stream
+    # the kernels run on give the device time per step inside the same region
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -105,19 +130,19 @@ def _run_rank(args, rank, world, local_rank):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    launch_us = e0.elapsed_time(e1) * 1e3 / args.steps
+    region_us = e0.elapsed_time(e1) * 1e3 / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     # per-launch kernel time (roofline) on the same kernel, stream and data
-    res = dict(elapsed=elapsed, kernel_us=launch_us,
-               event_pair_us=_kernel_time_us(env, step, actions, args.kernel_launches))
+    res = dict(elapsed=elapsed, region_us=region_us,
+               kernel_us=_gated_kernel_us(step, actions, args.kernel_launches))
     if args.rollout_steps > 0:
         res["rollout"] = _rollout_phase(env, args)
     if args.e2e_iters > 0:
-        res["end_to_end"] = _end_to_end(env, args)
+        res["end_to_end"] = _end_to_end(env, args, world)
     if rank == 0 and not args.no_configs:
         res["configs"] = {
             "config2_hover_4096": _kernel_rate(4096, "hover", None, dev, args.seed),
@@ -130,21 +155,7 @@ def _run_rank(args, rank, world, local_rank):
         big = QuadVecEnv(args.large_envs, env="hover", device=dev, seed=args.seed)
         big.reset()
         acts = [big.random_actions(k) for k in range(4)]
-        st = _quad_step_fn(big)
-        for k in range(5):
-            st(acts[k % 4].data_ptr())
-        gb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gb):
-            for k in range(20):
-                st(acts[k % 4].data_ptr())
-        gb.replay()
-        torch.cuda.synchronize()
-        e0.record()
-        for _ in range(5):
-            gb.replay()
-        e1.record()
-        torch.cuda.synchronize()
-        res["large_kernel_us"] = e0.elapsed_time(e1) * 1e3 / 100
+        res["large_kernel_us"] = _gated_kernel_us(_quad_step_fn(big), acts, 200)
         big.close()
     else:
         env.close()
@@ -160,26 +171,14 @@ def _kernel_rate(n, kind, wrapper, dev, seed) -> dict:
     st = _quad_step_fn(e)
     for k in range(50):
         st(acts[k % 4].data_ptr())
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        for k in range(20):
-            st(acts[k % 4].data_ptr())
-    g.replay()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        g.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / 200
+    us = _gated_kernel_us(st, acts, 200)
     e.close()
     bpe = BYTES_PER_ENV_STEP + (24 if wrapper else 0)
     return {"envs": n, "env": kind, "wrapper": wrapper, "kernel_us": us,
             "env_steps_per_s": n / (us * 1e-6), "achieved_GBs": bpe * n / (us * 1e-6) / 1e9}
 
 
-def _end_to_end(env, args) -> dict:
+def _end_to_end(env, args, world: int = 1) -> dict:
     """One full PPO iteration per SURVEY 8(d) config 3: rollout of n_steps (MFMA policy path) +
     GAE + the SB3-schedule update (n_epochs x n_minibatches Adam steps on the rollout buffer)."""
     from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
@@ -196,14 +195,21 @@ def _end_to_end(env, args) -> dict:
         torch.cuda.synchronize()
         t_train += time.perf_counter() - t0
         t_roll += rs.seconds
-    steps = args.e2e_iters * rs.env_steps
-    out = {"n_steps": cfg.n_steps, "n_epochs": cfg.n_epochs, "minibatches_per_epoch": cfg.n_minibatches,
+    steps = args.e2e_iters * rs.env_steps * world  # every rank's envs (config 4 at N = 8)
+    wall = t_roll + t_train
+    if world > 1:  # the slowest rank sets the whole job's time
+        t = torch.tensor([wall], dtype=torch.float64, device=env.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    out = {"world_size": world, "global_envs": env.num_envs * world,
+           "grad_allreduce": "one flat fp32 bucket (37,001 params) per optimizer step" if world > 1 else None,
+           "n_steps": cfg.n_steps, "n_epochs": cfg.n_epochs, "minibatches_per_epoch": cfg.n_minibatches,
            "minibatch": m.batch, "iterations": args.e2e_iters,
            "rollout_s": t_roll / args.e2e_iters, "train_s": t_train / args.e2e_iters,
            "update_path": "quad_ppo_grad (fused fwd+loss+bwd on MFMA) + quad_clip_adam"
            if m._learner is not None else "torch autograd",
            "ms_per_optimizer_step": 1e3 * t_train / args.e2e_iters / max(1, cfg.n_epochs * cfg.n_minibatches),
-           "env_steps_per_s": steps / (t_roll + t_train)}
+           "env_steps_per_s": steps / wall}
     if m._learner is not None:
         out["learner_kernel"] = _learner_kernel(m)
     del m
@@ -311,9 +317,30 @@ def _rollout_phase(env, args) -> dict:
     return out
 
 
-def _cpu_baseline(seconds: float) -> dict:
-    """The float64 CPU oracle (C restatement of HoverEnv + MuJoCo's step), one core, SB3
-    DummyVecEnv order (envs stepped one after another), random actions + auto-reset."""
+def _cpu_info() -> dict:
+    """The host the CPU baselines ran on: model name, logical CPUs, and the cores this process may
+    use (affinity mask, capped by OMP_NUM_THREADS: the GPU box grants 16 of a larger machine)."""
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        usable = min(usable, int(omp))
+    return {"model": model, "logical_cpus": os.cpu_count(), "usable_cores": max(1, usable)}
+
+
+def _cpu_baseline(seconds: float, threads: int = 1) -> dict:
+    """The float64 CPU oracle (C restatement of HoverEnv + MuJoCo's step), SB3 DummyVecEnv order
+    (envs stepped one after another), random actions + auto-reset. threads > 1: that many
+    independent 64-env batches stepped concurrently (ctypes drops the GIL), SubprocVecEnv-style."""
+    import threading
     from oracle import oracle as O
     n_envs = 64
     steps = 200
@@ -321,27 +348,33 @@ def _cpu_baseline(seconds: float) -> dict:
     O.bench_rollout(n_envs, steps, 0)
     dt = time.perf_counter() - t0
     steps = max(200, int(steps * seconds / max(dt, 1e-6)))
+    th = [threading.Thread(target=O.bench_rollout, args=(n_envs, steps, k)) for k in range(threads)]
     t0 = time.perf_counter()
-    O.bench_rollout(n_envs, steps, 0)
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
     dt = time.perf_counter() - t0
-    return {"value": n_envs * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+    cpu = _cpu_info()
+    return {"value": threads * n_envs * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ float64 C restatement (HoverEnv + MuJoCo-equivalent mj_step + SB3 "
-                      f"auto-reset), {n_envs} envs x {steps} steps sequential, random actions, "
-                      f"1 thread, {dt:.1f} s on {platform.processor() or platform.machine()}"}
+                      f"auto-reset), {threads} x {n_envs} envs x {steps} steps sequential per thread, "
+                      f"random actions, {threads} thread(s), {dt:.1f} s on {cpu['model']} "
+                      f"({cpu['logical_cpus']} logical CPUs, {cpu['usable_cores']} usable)"}
 
 
-def _cpu_baseline_ppo(seconds: float) -> dict:
+def _cpu_baseline_ppo(seconds: float, threads: int = 1) -> dict:
     """SURVEY config 1 on the host: the reference's CPU training loop shape -- train.py's 16 envs
     (HoverEnv + RateControlWrapper) stepped one after another (DummyVecEnv) through the float64 C
     oracle, a torch-CPU ActorCritic with SB3 semantics, GAE, and the SB3 update (n_epochs x
-    minibatches of 128 rows, clip_grad_norm_, Adam), 1 torch thread. Bounded: one rollout of
+    minibatches of 128 rows, clip_grad_norm_, Adam), `threads` torch threads. Bounded: one rollout of
     n_steps and as many update minibatches as fit the time budget, extrapolated per iteration."""
     import numpy as np
     from oracle import oracle as O
     from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
     from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig, ppo_loss
-    threads = torch.get_num_threads()
-    torch.set_num_threads(1)
+    old_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     try:
         cfg = PPOConfig()
         n_envs, T = 16, cfg.n_steps
@@ -401,13 +434,13 @@ def _cpu_baseline_ppo(seconds: float) -> dict:
             done += 1
         t_upd = (time.perf_counter() - t1) * steps_total / max(done, 1)
         it = t_roll + t_upd
-        return {"value": M / it, "unit": "env-steps/s (whole PPO iteration)", "cores": 1, "kind": "port",
+        return {"value": M / it, "unit": "env-steps/s (whole PPO iteration)", "cores": threads, "kind": "port",
                 "sample": f"train.py loop on the host: 16 oracle envs (HoverEnv + RateControlWrapper, DummyVecEnv "
                           f"order) x {T} steps + torch-CPU PPO update (SB3 schedule: {steps_total} Adam steps of "
-                          f"{B} rows; {done} timed, extrapolated), 1 thread; rollout {t_roll:.1f} s, update "
+                          f"{B} rows; {done} timed, extrapolated), {threads} torch thread(s); rollout {t_roll:.1f} s, update "
                           f"{t_upd:.1f} s per iteration"}
     finally:
-        torch.set_num_threads(threads)
+        torch.set_num_threads(old_threads)
 
 
 def _pmc_traffic(n_envs: int):
@@ -422,6 +455,65 @@ def _pmc_traffic(n_envs: int):
         return None
 
 
+def _pmc_issue(n_envs: int):
+    """The step kernel's counted issue roofline (rocprofv3 PMC: SQ_INSTS_VALU/SALU, SQ_BUSY_CYCLES,
+    GRBM_GUI_ACTIVE per launch) from the committed summary, if present (tools/pmc/issue_roofline.py)."""
+    path = os.path.join(REPO, "profiles", "pmc_issue.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get(str(n_envs))
+    except Exception:
+        return None
+
+
+def _launch_ranks(args) -> int:
+    """`--gpus N` without a torch.distributed launcher: start N rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set, one GPU each) and return their exit status. This parent never makes
+    a HIP call; if a rank fails, the others are stopped instead of waiting at a barrier."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def _check_launch(args, rank: int, world: int) -> None:
+    """--check-launch: the rank topology alone, on gloo (no GPU): every rank joins, the world
+    size matches --gpus, an all_reduce of the ranks reaches everyone; rank 0 prints one line."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        ranks_sum = float(t.item())
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        ranks_sum = 0.0
+    if rank == 0:
+        print(json.dumps({"check_launch": True, "n_gpus": world, "ranks_sum": ranks_sum,
+                          "global_envs": args.envs * world}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -433,21 +525,34 @@ def main():
     ap.add_argument("--action-batches", type=int, default=256)
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--large-envs", type=int, default=1 << 20)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=7.0)
     ap.add_argument("--rollout-steps", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-configs", action="store_true")
     ap.add_argument("--e2e-iters", type=int, default=1)
     ap.add_argument("--e2e-steps", type=int, default=1024)
     ap.add_argument("--e2e-epochs", type=int, default=20)
+    ap.add_argument("--check-launch", action="store_true",
+                    help="test the rank launch only (gloo, no GPU)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args))  # one child per GPU; this process never touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    if args.check_launch:
+        return _check_launch(args, rank, world)
     # rehearsal knob (tests only): run all ranks on one GPU over gloo, e.g. 2 ranks on a 1-GPU box
     rehearsal = os.environ.get("QUAD_BENCH_REHEARSAL") == "1"
     device_index = 0 if rehearsal else local_rank
+    if not rehearsal and torch.cuda.device_count() < local_rank + 1:
+        raise SystemExit(f"bench.py: rank {rank} needs GPU {local_rank}, "
+                         f"{torch.cuda.device_count()} visible")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(device_index)
@@ -455,6 +560,7 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", device_index))
+        assert dist.get_world_size() == args.gpus
 
     res = _run_rank(args, rank, world, device_index)
     if world > 1:
@@ -477,28 +583,32 @@ def main():
                                "envs/GPU), hipGraph replay",
                    "envs_per_gpu": args.envs, "global_envs": n_total,
                    "parallelism": f"env-shard x{world} (no data-path collective)"},
+        "device_us_per_step": res["region_us"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_step<HOVER,noCTBR>", "kernel_us": kus,
-                     "event_pair_us": res["event_pair_us"],
-                     "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs},
+                     "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs,
+                     "issue": _pmc_issue(args.envs)},
     }
     if "rollout" in res:
         line["rollout_phase"] = res["rollout"]
     if "end_to_end" in res:
-        e = dict(res["end_to_end"])
-        e["env_steps_per_s"] *= world
-        line["end_to_end"] = e
+        line["end_to_end"] = res["end_to_end"]
     if "configs" in res:
         line["configs"] = res["configs"]
     if "large_kernel_us" in res:
         lk = res["large_kernel_us"]
         line["large_batch"] = {"envs": args.large_envs, "kernel_us": lk,
                                "env_steps_per_s_kernel": args.large_envs / (lk * 1e-6),
-                               "achieved_GBs": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9}
-    if not args.no_cpu_baseline:
-        line["cpu_baseline"] = _cpu_baseline(args.cpu_seconds)
-        line["cpu_baseline_ppo"] = _cpu_baseline_ppo(args.cpu_seconds)
+                               "achieved_GBs": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9,
+                               "frac": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9 / HBM_PEAK_GBS}
+    if not args.no_cpu_baseline and world == 1:
+        cores = _cpu_info()["usable_cores"]
+        line["cpu_host"] = _cpu_info()
+        line["cpu_baseline"] = _cpu_baseline(args.cpu_seconds, 1)
+        line["cpu_baseline_all_cores"] = _cpu_baseline(args.cpu_seconds, cores)
+        line["cpu_baseline_ppo"] = _cpu_baseline_ppo(args.cpu_seconds, 1)
+        line["cpu_baseline_ppo_all_cores"] = _cpu_baseline_ppo(args.cpu_seconds, cores)
     print(json.dumps(line), flush=True)
 
 

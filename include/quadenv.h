@@ -166,6 +166,13 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
  * state12 (device [N,12] or NULL): the absolute QuadState vector (HoverEnv._state.vec()). */
 int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream);
 
+/* HoverEnv._is_terminated (hover_env.py:150-157; TrajectoryFollowEnv's bounds for that kind) on n
+ * caller-given absolute 12-D states (device [n,12], the QuadState vector: pos, roll/pitch/yaw, world
+ * velocity, body rates): terminated[i] = any non-finite component or any component outside the
+ * handle's inclusive termination bounds -- the predicate quad_step applies after each step.
+ * terminated: device [n] u8. Not defined for the brax kinds (QUAD_EINVAL). */
+int quad_terminated(QuadHandle* h, const float* state12, int32_t n, uint8_t* terminated, void* stream);
+
 /* action_space.sample() equivalent for synthetic rollouts: U[-1,1)^4 per env from
  * Philox(seed, global env id, step_index). actions: device [N,4]. */
 int quad_random_actions(QuadHandle* h, uint32_t step_index, float* actions, void* stream);

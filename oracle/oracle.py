@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libquadoracle.so")
 
 ENV_HOVER, ENV_TRAJ, ENV_BRAX_HOVER, ENV_BRAX_TRAJ = 0, 1, 2, 3
-WRAP_NONE, WRAP_CTBR = 0, 1
+WRAP_NONE, WRAP_CTBR, WRAP_RELPOS = 0, 1, 2
 
 
 class OracleOpt(C.Structure):
@@ -48,14 +48,15 @@ class OracleCfg(C.Structure):
 class OracleEnv(C.Structure):
     _fields_ = [("qpos", C.c_double * 11), ("qvel", C.c_double * 10), ("voltage", C.c_double),
                 ("target", C.c_float * 3), ("step_count", C.c_int32),
-                ("rate_int", C.c_double * 3), ("state12", C.c_float * 12)]
+                ("rate_int", C.c_double * 3), ("state12", C.c_float * 12),
+                ("prev_action", C.c_float * 4)]
 
 
 class OracleStepOut(C.Structure):
     _fields_ = [("obs", C.c_float * 12), ("reward", C.c_double), ("terminated", C.c_int32),
                 ("truncated", C.c_int32), ("state12", C.c_float * 12),
                 ("motor_commands", C.c_double * 4), ("voltage", C.c_double),
-                ("voltage_scale", C.c_double), ("env_action", C.c_float * 4)]
+                ("voltage_scale", C.c_double), ("env_action", C.c_float * 4), ("obs7", C.c_float * 7)]
 
 
 class OracleBraxCfg(C.Structure):
@@ -105,6 +106,7 @@ def lib():
         L.oracle_quat_to_euler.argtypes = [dp, dp]
         L.oracle_euler_to_quat.argtypes = [dp, dp]
         L.oracle_get_obs.argtypes = [C.POINTER(OracleCfg), C.POINTER(OracleEnv), fp]
+        L.oracle_relpos_obs.argtypes = [C.POINTER(OracleEnv), fp, fp]
         L.oracle_env_reset.argtypes = [C.POINTER(OracleCfg), C.POINTER(OracleEnv), fp, fp, fp]
         L.oracle_env_step.argtypes = [C.POINTER(OracleCfg), C.POINTER(OracleEnv), fp,
                                       C.POINTER(OracleStepOut)]
@@ -233,6 +235,13 @@ class Env:
         lib().oracle_env_reset(C.byref(self.cfg), C.byref(self.s), _fp(i12), _fp(t3), _fp(obs))
         return obs
 
+    def relpos_obs(self, obs12):
+        """RelPosActWrapper.observation of a base observation (wrappers.py:23-24)."""
+        o12 = np.ascontiguousarray(obs12, dtype=np.float32)
+        o7 = np.zeros(7, np.float32)
+        lib().oracle_relpos_obs(C.byref(self.s), _fp(o12), _fp(o7))
+        return o7
+
     def step(self, action):
         a = np.ascontiguousarray(action, dtype=np.float32)
         out = OracleStepOut()
@@ -249,13 +258,14 @@ class Env:
         return np.array(self.s.qvel[:], dtype=np.float64)
 
     def set_full_state(self, qpos, qvel, voltage, target, step_count, rate_int=(0, 0, 0),
-                       state12=None):
+                       state12=None, prev_action=(0, 0, 0, 0)):
         self.s.qpos[:] = [float(x) for x in qpos]
         self.s.qvel[:] = [float(x) for x in qvel]
         self.s.voltage = float(voltage)
         self.s.target[:] = [float(x) for x in np.asarray(target, np.float32)]
         self.s.step_count = int(step_count)
         self.s.rate_int[:] = [float(x) for x in rate_int]
+        self.s.prev_action[:] = [float(x) for x in np.asarray(prev_action, np.float32)]
         if state12 is None:
             obs = np.zeros(12, np.float32)
             lib().oracle_get_obs(C.byref(self.cfg), C.byref(self.s), _fp(obs))
@@ -269,7 +279,7 @@ def out_to_dict(o: OracleStepOut) -> dict:
                 state12=np.array(o.state12[:], np.float32),
                 motor_commands=np.array(o.motor_commands[:], np.float64),
                 voltage=float(o.voltage), voltage_scale=float(o.voltage_scale),
-                env_action=np.array(o.env_action[:], np.float32))
+                env_action=np.array(o.env_action[:], np.float32), obs7=np.array(o.obs7[:], np.float32))
 
 
 class BraxEnv:

@@ -661,6 +661,7 @@ void oracle_env_reset(const OracleCfg* cfg, OracleEnv* env, const float init12[1
   env->step_count = 0;
   env->voltage = cfg->nominal_voltage;
   for (int i = 0; i < 3; i++) env->rate_int[i] = 0.0; /* rate_wrapper.py:110 */
+  for (int i = 0; i < 4; i++) env->prev_action[i] = 0.0f; /* hover_env.py:212 */
   /* QuadState.get_mujoco_state (state.py:48-65) + HoverEnv.set_state (hover_env.py:143-148) */
   const double e[3] = {init12[3], init12[4], init12[5]};
   for (int i = 0; i < 3; i++) env->qpos[i] = init12[i];
@@ -693,6 +694,9 @@ int oracle_env_step(const OracleCfg* cfg, OracleEnv* env, const float action[4],
     for (int k = 1; k < 4; k++) a[k] = action[k];
   }
   memcpy(out->env_action, a, sizeof a);
+  /* self._prev_action = np.array(action, dtype=np.float32) (hover_env.py:166): the action the
+   * base env receives (after RateControlWrapper.action when that wrapper is on) */
+  memcpy(env->prev_action, a, sizeof a);
   /* denormalize (normalization.py:20-30), float32 */
   float phys[4];
   for (int k = 0; k < 4; k++) {
@@ -745,7 +749,14 @@ int oracle_env_step(const OracleCfg* cfg, OracleEnv* env, const float action[4],
   memcpy(out->motor_commands, F, sizeof F);
   out->voltage = env->voltage;
   out->voltage_scale = vs;
+  oracle_relpos_obs(env, out->obs, out->obs7);
   return 0;
+}
+
+void oracle_relpos_obs(const OracleEnv* env, const float obs12[12], float obs7[7]) {
+  /* np.concatenate([obs[0:3], self.unwrapped._prev_action]).astype(np.float32) */
+  for (int i = 0; i < 3; i++) obs7[i] = obs12[i];
+  for (int i = 0; i < 4; i++) obs7[3 + i] = env->prev_action[i];
 }
 
 void oracle_env_step_batch(const OracleCfg* cfg, OracleEnv* envs, int32_t n,

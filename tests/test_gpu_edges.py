@@ -1,0 +1,155 @@
+"""GPU edge cases of the termination predicate and RelPosActWrapper, through the C ABI, bit-exact
+against the reference's own goldens (tests/golden, tools/gen_golden.py) and the oracle.
+
+* `quad_terminated` runs the step kernels' `terminated_of` on given 12-D states: every row of
+  golden_termination.npz (inclusive bounds, nextafter neighbours, NaN, +-Inf, random) for the
+  hover and trajectory bounds (hover_env.py:54-57,150-157; trajectory_follow_env.py:60-63).
+* The same edges through a whole `quad_step`: a zero-dynamics config (timestep 0, no gravity, no
+  fluid, zero thrust) leaves the injected state unchanged, so the step's own termination test
+  sees exactly the golden state (position / velocity / rate edges with zero attitude), and 180
+  degree attitudes reach roll / yaw = +-f32(pi) exactly. NaN / Inf states cannot pass through a
+  step (MuJoCo's mj_checkPos/Vel resets them before the env looks), so they are covered by
+  quad_terminated only.
+* `k_step_relpos` (QUAD_WRAP_RELPOS, wrappers.py:13-25) against the oracle's RELPOS kind, which is
+  pinned bit-exact to the reference wrapper (test_oracle_golden.py), incl. auto-reset rows.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _env(n, env="hover", wrapper=None, **kw):
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    return QuadVecEnv(n, env=env, wrapper=wrapper, device="cuda:0", **kw)
+
+
+def parity_ok(got, ref, rtol=1e-5, atol=1e-6):
+    got = np.asarray(got, np.float64); ref = np.asarray(ref, np.float64)
+    return np.all((np.isnan(got) & np.isnan(ref)) | (np.abs(got - ref) <= rtol * np.abs(ref) + atol), axis=-1)
+
+
+@pytest.mark.parametrize("env_name,key", [("hover", "hover"), ("trajectory", "traj")])
+def test_termination_predicate_bit_exact(golden_dir, env_name, key):
+    d = np.load(os.path.join(golden_dir, "golden_termination.npz"))
+    s = torch.from_numpy(d[f"{key}_states"]).cuda()
+    env = _env(8, env_name)
+    got = env.is_terminated(s).cpu().numpy()
+    assert np.array_equal(got, d[f"{key}_terminated"])
+    assert got.sum() > 0 and (~got).sum() > 0
+    env.close()
+
+
+ZERO_DYN = dict(timestep=0.0, gravity=[0.0, 0.0, 0.0], density=0.0, viscosity=0.0)
+
+
+@pytest.mark.parametrize("env_name,key,kind", [("hover", "hover", O.ENV_HOVER), ("trajectory", "traj", O.ENV_TRAJ)])
+def test_termination_edges_through_step(golden_dir, env_name, key, kind):
+    d = np.load(os.path.join(golden_dir, "golden_termination.npz"))
+    S, T = d[f"{key}_states"], d[f"{key}_terminated"]
+    rows = [i for i in range(len(S)) if np.all(np.isfinite(S[i])) and np.all(S[i][3:6] == 0)]
+    extra = [(0.0, 1.0, 0.0, 0.0), (0.0, -1.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0), (0.0, 0.0, 0.0, -1.0),
+             (0.0, 0.0, 1.0, 0.0), (1.0, 0.0, 0.0, 0.0)]  # 180 degree turns: roll / yaw at +-f32(pi)
+    n = len(rows) + len(extra)
+    qpos = np.zeros((n, 11), np.float32); qvel = np.zeros((n, 10), np.float32)
+    for j, i in enumerate(rows):
+        qpos[j, :3] = S[i][:3]; qpos[j, 3] = 1.0
+        qvel[j, :3] = S[i][6:9]; qvel[j, 3:6] = S[i][9:12]
+    for j, q in enumerate(extra):
+        qpos[len(rows) + j, :3] = (0.0, 0.0, 1.0); qpos[len(rows) + j, 3:7] = q
+    step = np.full(n, 100, np.int32)
+    step[::3] = 511 if kind == O.ENV_HOVER else 2047   # truncation together with termination
+    cfg_max = 512 if kind == O.ENV_HOVER else 2048
+    env = _env(n, env_name, auto_reset=False, cfg_overrides=ZERO_DYN)
+    env.set_state(qpos=qpos, qvel=qvel, voltage=np.full(n, 8.4, np.float32), target=np.zeros((n, 3), np.float32),
+                  step_count=step, rate_int=np.zeros((n, 3), np.float32))
+    act = torch.tensor([[-1.0, 0.0, 0.0, 0.0]], device="cuda:0").repeat(n, 1)  # zero thrust and torque
+    obs, rew, te, tr, inf = env.step(act, info="full")
+    s12 = inf["state"].cpu().numpy(); te = te.cpu().numpy(); tr = tr.cpu().numpy()
+    post = env.get_state()
+    assert np.array_equal(post["qpos"], qpos) and np.array_equal(post["qvel"], qvel)  # nothing moved
+    for j, i in enumerate(rows):
+        assert np.array_equal(s12[j], S[i]), (i, s12[j], S[i])
+        assert te[j] == T[i], (i, S[i])
+    cfg = O.default_cfg(kind, O.WRAP_NONE)
+    lo, hi = np.array(cfg.term_low[:], np.float32), np.array(cfg.term_high[:], np.float32)
+    pi32 = np.float32(np.pi)
+    seen = set()
+    for j in range(len(rows), n):
+        e = O.Env(cfg=cfg)
+        e.set_full_state(qpos[j], qvel[j], 8.4, (0, 0, 0), 0)
+        assert np.array_equal(s12[j], np.array(e.s.state12[:], np.float32)), (j, s12[j])
+        ref_te = (not np.isfinite(s12[j]).all()) or not ((s12[j] >= lo) & (s12[j] <= hi)).all()
+        assert te[j] == ref_te
+        seen |= {float(x) for x in s12[j][3:6] if abs(x) == pi32}
+    assert seen == {float(pi32), float(-pi32)}  # both inclusive attitude edges were exercised
+    assert np.array_equal(tr, step + 1 >= cfg_max)
+    assert (te & tr).any()                       # term and trunc can both be true
+    env.close()
+
+
+@pytest.mark.parametrize("name,env_name,kind,max_steps", [("relpos_steps", "hover", O.ENV_HOVER, 60),
+                                                         ("traj_relpos_steps", "trajectory", O.ENV_TRAJ, 50)])
+def test_relpos_step_matches_oracle_and_reference(golden_dir, name, env_name, kind, max_steps):
+    d = np.load(os.path.join(golden_dir, f"golden_{name}.npz"))
+    n = len(d["action"])
+    env = _env(n, env_name, "RelPosActWrapper", auto_reset=False, max_episode_steps=max_steps)
+    st = dict(qpos=d["pre_qpos"].astype(np.float32), qvel=d["pre_qvel"].astype(np.float32),
+              voltage=d["pre_voltage"].astype(np.float32), target=d["pre_target"],
+              step_count=d["pre_step"].astype(np.int32), prev_action=d["pre_prev_action"])
+    env.set_state(**st)
+    obs, rew, te, tr, inf = env.step(torch.from_numpy(d["action"]).cuda(), info="full")
+    obs = obs.cpu().numpy(); te = te.cpu().numpy(); tr = tr.cpu().numpy(); rew = rew.cpu().numpy()
+    assert obs.shape == (n, 7)
+    cfg = O.default_cfg(kind, O.WRAP_RELPOS)
+    cfg.max_episode_steps = max_steps
+    for i in range(n):
+        e = O.Env(cfg=cfg)
+        e.set_full_state(st["qpos"][i], st["qvel"][i], st["voltage"][i], st["target"][i], st["step_count"][i],
+                         (0, 0, 0), None, st["prev_action"][i])
+        o = O.out_to_dict(e.step(d["action"][i]))
+        assert te[i] == o["terminated"] == d["terminated"][i] and tr[i] == o["truncated"] == d["truncated"][i], i
+        assert parity_ok(obs[i], o["obs7"]) and parity_ok(obs[i], d["obs"][i]), (i, obs[i], o["obs7"])
+        assert np.array_equal(obs[i][3:], d["obs"][i][3:])  # the previous action is copied exactly
+        assert parity_ok(rew[i], o["reward"]), i
+    g = env.get_state()
+    assert np.array_equal(g["prev_action"], d["action"])
+    env.close()
+
+
+@pytest.mark.parametrize("env_name,kind", [("hover", O.ENV_HOVER), ("trajectory", O.ENV_TRAJ)])
+def test_relpos_auto_reset_matches_oracle(env_name, kind):
+    """SB3 auto-reset under RelPosActWrapper: terminal_observation = the wrapper's obs7 of the
+    finishing step (prev action = the action just taken); the returned obs = obs7 of the reset
+    (Philox draws of the episode counter, prev action zeros), bit-exact with the oracle."""
+    n = 4096
+    env = _env(n, env_name, "RelPosActWrapper", seed=31, max_episode_steps=7)
+    env.reset()
+    cfg = O.default_cfg(kind, O.WRAP_RELPOS)
+    cfg.max_episode_steps = 7
+    checked = 0
+    for k in range(16):
+        pre = env.get_state()
+        acts = env.random_actions(k)
+        obs, rew, te, tr, inf = env.step(acts)
+        te = te.cpu().numpy(); tr = tr.cpu().numpy(); obs = obs.cpu().numpy(); a = acts.cpu().numpy()
+        tobs = inf["terminal_observation"].cpu().numpy()
+        for i in np.nonzero(te | tr)[0][:40]:
+            e = O.Env(cfg=cfg)
+            e.set_full_state(pre["qpos"][i], pre["qvel"][i], pre["voltage"][i], pre["target"][i],
+                             pre["step_count"][i], (0, 0, 0), None, pre["prev_action"][i])
+            o = O.out_to_dict(e.step(a[i]))
+            assert parity_ok(tobs[i], o["obs7"]) and np.array_equal(tobs[i][3:], a[i]), i
+            i12, t3 = O.reset_draw(cfg, 31, i, pre["episode"][i])
+            r = O.Env(cfg=cfg)
+            assert np.array_equal(obs[i], r.relpos_obs(r.reset_with(i12, t3))), i
+            checked += 1
+        live = ~(te | tr)
+        assert np.array_equal(obs[live][:, 3:], a[live])
+    assert checked > 50
+    env.close()

@@ -174,6 +174,11 @@ def test_fused_clip_adam_matches_torch(max_norm):
     oa.step()
 
 
+DP_ENVS, DP_STEPS = 2048, 64
+DP_BUFFERS = ("buf_obs", "buf_act", "buf_logp", "buf_val", "buf_rew", "buf_start", "buf_adv", "buf_ret",
+              "last_obs", "last_start")
+
+
 def _dp_worker(rank, world, port, q):
     try:
         import os
@@ -182,19 +187,20 @@ def _dp_worker(rank, world, port, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)  # both ranks share cuda:0 here
         from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
         from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
-        n = 2048
+        n = DP_ENVS
         env = QuadVecEnv(n, env="hover", device="cuda:0", seed=5, env_id_base=rank * n)
-        algo = PPO(env, PPOConfig(n_steps=16, n_minibatches=4, n_epochs=1), seed=3)
+        algo = PPO(env, PPOConfig(n_steps=DP_STEPS, n_minibatches=4, n_epochs=1), seed=3)
         assert algo._learner is not None and algo.world == world
         p0 = torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()]).cpu()
         algo.collect_rollouts()
+        bufs = {k: getattr(algo, k).cpu().numpy() for k in DP_BUFFERS}
         st = algo.train()
         p1 = torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()]).cpu()
-        q.put((rank, p0.numpy(), p1.numpy(), st["n"]))
+        q.put((rank, p0.numpy(), p1.numpy(), st["n"], bufs))
         env.close()
         dist.destroy_process_group()
     except Exception as e:  # report instead of leaving the parent waiting
-        q.put((rank, repr(e), None, None))
+        q.put((rank, repr(e), None, None, None))
 
 
 def test_fused_update_two_ranks_stay_in_sync():
@@ -208,12 +214,31 @@ def test_fused_update_two_ranks_stay_in_sync():
     procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = {r: (a, b, n) for r, a, b, n in (q.get(timeout=240) for _ in range(2))}
+    res = {r: (a, b, n, bufs) for r, a, b, n, bufs in (q.get(timeout=240) for _ in range(2))}
     for p in procs:
         p.join(timeout=60)
-    assert all(b is not None for _, b, _ in res.values()), res
-    (a0, b0, n0), (a1, b1, n1) = res[0], res[1]
+    assert all(b is not None for _, b, _, _ in res.values()), res
+    (a0, b0, n0, _), (a1, b1, n1, _) = res[0], res[1]
     assert n0 == n1 == 4
     assert np.array_equal(a0, a1)                  # same init
     assert np.abs(b0 - a0).max() > 1e-5            # the update moved the policy
     np.testing.assert_array_equal(b0, b1)          # ... identically on both ranks
+    # SURVEY 8(e) / DESIGN 5: rank r's shard is bit-identical to the same global env ids run in
+    # one process -- the rollout (policy noise, auto-resets, timeout bootstraps, GAE) of the two
+    # ranks concatenated equals one process stepping all 2 x DP_ENVS envs
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
+    env = QuadVecEnv(2 * DP_ENVS, env="hover", device="cuda:0", seed=5, env_id_base=0)
+    one = PPO(env, PPOConfig(n_steps=DP_STEPS, n_minibatches=4, n_epochs=1), seed=3)
+    one.collect_rollouts()
+    resets = 0
+    for k in DP_BUFFERS:
+        full = getattr(one, k).cpu().numpy()
+        axis = 0 if k.startswith("last") else 1
+        for r in range(2):
+            shard = np.take(full, range(r * DP_ENVS, (r + 1) * DP_ENVS), axis=axis)
+            np.testing.assert_array_equal(res[r][3][k], shard, err_msg=f"{k} rank {r}")
+        if k == "buf_start":
+            resets = int(full[1:].sum())
+    assert resets > 0  # the window covers auto-resets
+    env.close()

@@ -83,3 +83,26 @@ def test_termination_matches_reference(golden_dir):
         for s, t in zip(d[f"{name}_states"], d[f"{name}_terminated"]):
             mine = (not np.isfinite(s).all()) or (not ((s >= lo) & (s <= hi)).all())
             assert mine == bool(t)
+
+
+@pytest.mark.parametrize("name,kind", [("relpos_steps", O.ENV_HOVER), ("traj_relpos_steps", O.ENV_TRAJ)])
+def test_relpos_wrapper_matches_reference(golden_dir, name, kind):
+    """RelPosActWrapper(HoverEnv / TrajectoryFollowEnv) (envs/wrappers.py:13-25), the reference's
+    wrapper executed unmodified: obs7 = [obs12[0:3], _prev_action] bit-exact for every step (the
+    previous action is the one just taken) and every reset (zeros, hover_env.py:212)."""
+    d = np.load(os.path.join(golden_dir, f"golden_{name}.npz"))
+    cfg = O.default_cfg(kind, O.WRAP_RELPOS)
+    cfg.max_episode_steps = 60 if kind == O.ENV_HOVER else 50
+    env = O.Env(cfg=cfg)
+    for t in range(len(d["action"])):
+        env.set_full_state(d["pre_qpos"][t], d["pre_qvel"][t], d["pre_voltage"][t], d["pre_target"][t],
+                           d["pre_step"][t], (0, 0, 0), d["pre_state12"][t], d["pre_prev_action"][t])
+        o = O.out_to_dict(env.step(d["action"][t]))
+        assert np.array_equal(o["obs7"], d["obs"][t]), (name, t)
+        assert o["terminated"] == d["terminated"][t] and o["truncated"] == d["truncated"][t]
+        np.testing.assert_allclose(o["reward"], d["reward"][t], rtol=1e-13, atol=1e-15)
+    assert d["terminated"].any() or d["truncated"].any()
+    for i in range(len(d["reset_init12"])):
+        e = O.Env(cfg=cfg)
+        obs = e.reset_with(d["reset_init12"][i], d["reset_target3"][i])
+        assert np.array_equal(e.relpos_obs(obs), d["reset_obs"][i]), (name, i)

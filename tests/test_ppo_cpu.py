@@ -102,6 +102,21 @@ def _worker_body(rank, world, port, q):
     flat = torch.zeros_like(local)
     allreduce_mean_(list(p.parameters()), flat, world)
     avg = torch.cat([x.grad.reshape(-1) for x in p.parameters()])
+    # the same gradient with the .grad tensors bound to the bucket: autograd accumulates into the
+    # views, the all-reduce runs in place, and the result is the same average
+    from uav_reinforcement_learning_control_amd.ppo.ppo import _bucket_bound, bind_grad_bucket
+    params = list(p.parameters())
+    bucket = torch.zeros_like(local)
+    bind_grad_bucket(params, bucket)
+    for x in params:
+        x.grad.zero_()
+    mean, v = p.forward_heads(obs)
+    loss = v.pow(2).mean() + mean.pow(2).mean() + (rank + 1.0) * p.log_std.pow(2).sum() + p.entropy()
+    loss.backward()
+    assert _bucket_bound(params, bucket)
+    assert torch.equal(bucket, local)
+    allreduce_mean_(params, bucket, world)
+    assert _bucket_bound(params, bucket) and torch.equal(bucket, avg)
     q.put((rank, local.numpy(), avg.numpy()))
     dist.destroy_process_group()
 

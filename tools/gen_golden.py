@@ -123,21 +123,26 @@ def termination_fixture():
     return out
 
 
-def rollout_fixture(kind: str, wrapper: bool, n_steps: int, seeds, max_episode_steps=None,
+def rollout_fixture(kind: str, wrapper, n_steps: int, seeds, max_episode_steps=None,
                     action_mode="mixed"):
+    """wrapper: False/None, True (RateControlWrapper) or "relpos" (RelPosActWrapper: the recorded
+    obs / reset_obs are then the wrapper's 7-D observations, plus pre_prev_action)."""
     from envs.hover_env import HoverEnv
     from envs.rate_wrapper import RateControlWrapper
     from envs.trajectory_follow_env import TrajectoryFollowEnv
+    from envs.wrappers import RelPosActWrapper
 
     kw = {} if max_episode_steps is None else dict(max_episode_steps=max_episode_steps)
     base = HoverEnv(**kw) if kind == "hover" else TrajectoryFollowEnv(**kw)
-    env = RateControlWrapper(base) if wrapper else base
+    relpos = wrapper == "relpos"
+    env = RelPosActWrapper(base) if relpos else RateControlWrapper(base) if wrapper else base
+    wrapper = bool(wrapper) and not relpos  # the CTBR integrator fields below
     u = env.unwrapped
     arng = np.random.default_rng(99)
     rec = {k: [] for k in ("pre_qpos", "pre_qvel", "pre_voltage", "pre_target", "pre_step",
                            "pre_state12", "pre_rate_int", "action", "obs", "reward", "terminated",
                            "truncated", "motor", "voltage", "vscale", "post_qpos", "post_qvel",
-                           "post_state12", "post_rate_int", "info_state")}
+                           "post_state12", "post_rate_int", "info_state", "pre_prev_action")}
     resets = {k: [] for k in ("init12", "target3", "obs", "qpos", "qvel", "state12")}
 
     def do_reset(seed):
@@ -191,6 +196,7 @@ def rollout_fixture(kind: str, wrapper: bool, n_steps: int, seeds, max_episode_s
         rec["pre_step"].append(u._step_count)
         rec["pre_state12"].append(u._state.vec())
         rec["pre_rate_int"].append(env._rate_int_torque.copy() if wrapper else np.zeros(3))
+        rec["pre_prev_action"].append(u._prev_action.copy())
         rec["action"].append(a)
         obs, r, te, tr, info = env.step(a)
         rec["obs"].append(obs)
@@ -209,7 +215,7 @@ def rollout_fixture(kind: str, wrapper: bool, n_steps: int, seeds, max_episode_s
             do_reset(seeds.pop(0) if seeds else None)
     out = {k: np.array(v) for k, v in rec.items()}
     out.update({"reset_" + k: np.array(v) for k, v in resets.items()})
-    for k in ("action", "obs", "pre_target", "pre_state12", "post_state12", "info_state",
+    for k in ("action", "obs", "pre_target", "pre_state12", "pre_prev_action", "post_state12", "info_state",
               "reset_init12", "reset_target3", "reset_obs", "reset_state12"):
         out[k] = out[k].astype(np.float32)
     return out
@@ -237,7 +243,11 @@ def main():
     _setup()
     os.makedirs(args.out, exist_ok=True)
     if args.only:
-        lazy = {"golden_trajectories.npz": trajectories_fixture}
+        lazy = {"golden_trajectories.npz": trajectories_fixture,
+                "golden_relpos_steps.npz": lambda: rollout_fixture("hover", "relpos", 400, range(4000, 4100),
+                                                                   max_episode_steps=60),
+                "golden_traj_relpos_steps.npz": lambda: rollout_fixture("traj", "relpos", 300, range(5000, 5100),
+                                                                        max_episode_steps=50)}
         for name in args.only.split(","):
             d = lazy[name]()
             np.savez_compressed(os.path.join(args.out, name), **d)
@@ -255,6 +265,9 @@ def main():
         "golden_ctbr_steps.npz": rollout_fixture("hover", True, 1500, range(1000, 1300)),
         "golden_traj_ctbr_steps.npz": rollout_fixture("traj", True, 800, range(2000, 2300)),
         "golden_traj_steps.npz": rollout_fixture("traj", False, 400, range(3000, 3300)),
+        "golden_relpos_steps.npz": rollout_fixture("hover", "relpos", 400, range(4000, 4100), max_episode_steps=60),
+        "golden_traj_relpos_steps.npz": rollout_fixture("traj", "relpos", 300, range(5000, 5100),
+                                                        max_episode_steps=50),
     }
     for name, d in fx.items():
         path = os.path.join(args.out, name)

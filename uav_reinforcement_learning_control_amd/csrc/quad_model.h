@@ -156,6 +156,9 @@ inline bool make_phys_consts(const QuadCfg& cfg, PhysConstsD& c, const char** wh
   c.dt = cfg.timestep;
   c.ctrl_lo = md.ctrl_lo;
   c.ctrl_hi = md.ctrl_hi;
+  // env_step and k_rollout clamp the (non-negative) motor forces with physics_step<.., F_NONNEG>,
+  // which applies only the upper ctrlrange bound: that is exact only while ctrl_lo <= 0
+  if (!(c.ctrl_lo <= 0.0 && c.ctrl_hi >= c.ctrl_lo)) { *why = "ctrlrange must satisfy lo <= 0 <= hi"; return false; }
   // mixer inverse (Gauss-Jordan, partial pivoting) of A = [[1,1,1,1],[-l,-l,l,l],[-l,l,l,-l],[k,-k,k,-k]]
   const double l = cfg.arm_length, k = cfg.yaw_coeff;
   double M[4][8] = {{1, 1, 1, 1}, {-l, -l, l, l}, {-l, l, l, -l}, {k, -k, k, -k}};

@@ -458,7 +458,8 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
     if (F_NONNEG)  // ctrl_lo <= 0 <= f: only the upper bound can bind
       F[i] = f > c.ctrl_hi ? c.ctrl_hi : f;
     else
-      F[i] = clipn(f, c.ctrl_lo, c.ctrl_hi);  // (flat selects; f is never NaN here)
+      F[i] = clipn(f, c.ctrl_lo, c.ctrl_hi);  // flat selects; a NaN ctrl (CHECKS = false, the brax
+                                              // kinds: mjx has no bad-ctrl zeroing) passes through
   }
   T Fsum = T(F[0] + F[1] + F[2] + F[3]);
   T taum[3] = {T(c.syd[0] * F[0] + c.syd[1] * F[1] + c.syd[2] * F[2] + c.syd[3] * F[3]),

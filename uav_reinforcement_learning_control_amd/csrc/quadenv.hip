@@ -842,6 +842,19 @@ __global__ __launch_bounds__(BLOCK) void k_observe(KParams p, float* __restrict_
   }
 }
 
+// HoverEnv._is_terminated (hover_env.py:150-157) on caller-given absolute 12-D states: the step
+// kernels' own predicate (terminated_of), bounds from the handle's constants
+__global__ __launch_bounds__(BLOCK) void k_terminated(const KConsts<float>* __restrict__ kc,
+                                                      const float* __restrict__ s12, int32_t n,
+                                                      uint8_t* __restrict__ out) {
+  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  float s[12];
+#pragma unroll
+  for (int j = 0; j < 12; j++) s[j] = s12[size_t(i) * 12 + j];
+  out[i] = terminated_of(*kc, s) ? 1 : 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // batched waypoint evaluation (evaluate.py:440-612)
 template <bool RELPOS>
@@ -1308,6 +1321,18 @@ int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream) {
   else
     hipLaunchKernelGGL(k_observe<false>, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
                        h->kp, obs, state12);
+  HIP_TRY(hipGetLastError());
+  return QUAD_OK;
+}
+
+int quad_terminated(QuadHandle* h, const float* state12, int32_t n, uint8_t* terminated, void* stream) {
+  if (!h || !state12 || !terminated) return fail(QUAD_EINVAL, "handle/state12/terminated is NULL");
+  if (h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) return fail(QUAD_EINVAL, "the brax env kinds have no QuadState bounds");
+  if (n < 0) return fail(QUAD_EINVAL, "n must be >= 0");
+  if (n == 0) return QUAD_OK;
+  DeviceGuard g(h->device);
+  hipLaunchKernelGGL(k_terminated, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
+                     h->kdev, state12, n, terminated);
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
 }

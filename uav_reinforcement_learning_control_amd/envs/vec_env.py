@@ -183,6 +183,19 @@ class QuadVecEnv:
                                      self._stream()), "quad_observe")
         return (out, self.state12) if state else out
 
+    def is_terminated(self, state12: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """HoverEnv._is_terminated (hover_env.py:150-157) for given absolute 12-D states [M,12]
+        (float32 on this env's GPU): the step kernels' own predicate with this env's bounds."""
+        if self.brax:
+            raise ValueError("the brax kinds have no QuadState bounds")
+        m = int(state12.shape[0])
+        self._check(state12, (m, 12), torch.float32)
+        out = torch.empty(m, dtype=torch.bool, device=self.device) if out is None else out
+        self._check(out, (m,), torch.bool)
+        N.check(N.lib().quad_terminated(self._h, _ptr(state12), m, _ptr(out), self._stream()),
+                "quad_terminated")
+        return out
+
     def random_actions(self, step_index: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """action_space.sample() for every env (Philox(seed, env id, step_index))."""
         out = torch.empty(self.num_envs, 4, dtype=torch.float32, device=self.device) \

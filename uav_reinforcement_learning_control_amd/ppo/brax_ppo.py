@@ -244,6 +244,8 @@ class BraxPPO:
         self._obs = None
         self._ep_ret = torch.zeros(c.num_envs, device=self.device)
         self._flat = torch.zeros(sum(p.numel() for p in self.net.parameters()), device=self.device)
+        from .ppo import bind_grad_bucket
+        bind_grad_bucket(list(self.net.parameters()), self._flat)  # in-place all-reduce
 
     @torch.no_grad()
     def _unrolls(self):

@@ -91,6 +91,13 @@ class FusedPolicy:
                             epilogue=C.pointer(epilogue) if epilogue is not None else None)
         N.check(N.lib().quad_policy_act(_p(self.packed), C.byref(a), n, self._stream()), "quad_policy_act")
 
+    def value(self, obs: torch.Tensor, out: torch.Tensor, scratch: torch.Tensor) -> torch.Tensor:
+        """V(obs) [N] into out ([1, N]) on the MFMA kernel: per-row results do not depend on the
+        batch (no GEMM tiling choice), so a rank's shard bootstraps exactly as in one process.
+        `scratch` ([N, 4]) receives the deterministic actions."""
+        self.act(obs, scratch, value=out, rows=1, deterministic=True)
+        return out[0]
+
     def make_epilogue(self, reward, terminated, truncated, terminal_obs, buf_rew, last_start, ep_ret,
                       ep_len, stats, rows: int, gamma: float) -> N.QuadRolloutPost:
         """The QuadRolloutPost of a rollout (buffers are referenced, not copied: keep them alive)."""

@@ -72,21 +72,51 @@ def ppo_loss(policy: ActorCritic, obs, act, logp_old, adv, ret, cfg: PPOConfig):
     return loss, pg, vf, ent, clip_frac
 
 
+def bind_grad_bucket(params, flat: torch.Tensor) -> None:
+    """Make every parameter's .grad a view of one flat fp32 bucket (parameter order), so the
+    gradient kernels (quad_ppo_grad's reduction, autograd's in-place accumulation) write straight
+    into the buffer the all-reduce sends: no copies around the collective."""
+    off = 0
+    for p in params:
+        k = p.numel()
+        p.grad = flat[off:off + k].view_as(p)
+        off += k
+    if off != flat.numel():
+        raise ValueError("bucket size does not match the parameters")
+
+
+def _bucket_bound(params, flat: torch.Tensor) -> bool:
+    base, off = flat.data_ptr(), 0
+    for p in params:
+        g = p.grad
+        if g is None or g.data_ptr() != base + 4 * off or not g.is_contiguous():
+            return False
+        off += p.numel()
+    return True
+
+
 def allreduce_mean_(params, flat: torch.Tensor, world: int) -> None:
-    """Average the gradients of `params` over ranks with ONE all_reduce of a flat fp32 bucket."""
-    grads = [p.grad for p in params]
-    off = 0
-    for g in grads:
-        k = g.numel()
-        flat[off:off + k].copy_(g.reshape(-1))
-        off += k
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
-    flat.div_(world)
-    off = 0
-    for g in grads:
-        k = g.numel()
-        g.copy_(flat[off:off + k].view_as(g))
-        off += k
+    """Average the gradients of `params` over ranks with ONE all_reduce of a flat fp32 bucket.
+    With the .grad tensors bound to the bucket (bind_grad_bucket) the collective runs in place;
+    otherwise (a caller replaced a .grad) they are copied in and out."""
+    bound = _bucket_bound(params, flat)
+    if not bound:
+        off = 0
+        for p in params:
+            k = p.numel()
+            flat[off:off + k].copy_(p.grad.reshape(-1))
+            off += k
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(flat, op=dist.ReduceOp.AVG)   # RCCL: the mean in the collective itself
+    else:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM)   # gloo has no AVG
+        flat.div_(world)
+    if not bound:
+        off = 0
+        for p in params:
+            k = p.numel()
+            p.grad.copy_(flat[off:off + k].view_as(p))
+            off += k
 
 
 @dataclass
@@ -135,8 +165,10 @@ class PPO:
         else:
             self.batch = max(1, total // self.cfg.n_minibatches)
         self._flat = torch.zeros(sum(p.numel() for p in self.params), **f32)
+        bind_grad_bucket(self.params, self._flat)  # .grad tensors are views of the all-reduce bucket
         self._t = torch.zeros(1, dtype=torch.long, device=self.device)
         self._act_env = torch.zeros(n, 4, **f32)
+        self._last_v = torch.zeros(1, n, **f32)
         self._done_stats = torch.zeros(3, dtype=torch.float64, device=self.device)
         self._graph = None
         # fused path: cursor {t, pending} (buffer row = t % n_steps; t keys the action noise),
@@ -251,7 +283,7 @@ class PPO:
         if self._fp is not None:
             self._fp.post(self._epi, self._cursor)   # finish the last step
             self._done_stats.copy_(self._slots.sum(0))
-        last_v = pol.value(self.last_obs)
+        last_v = self._bootstrap_value()
         gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
             cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
         torch.cuda.synchronize(self.device)
@@ -281,7 +313,7 @@ class PPO:
             s += k
         self._t_host += cfg.n_steps
         self._done_stats.copy_(self._slots.sum(0))
-        last_v = pol.value(self.last_obs)
+        last_v = self._bootstrap_value()
         gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
             cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
         torch.cuda.synchronize(self.device)
@@ -291,6 +323,12 @@ class PPO:
         return RolloutStats(episodes=int(c), mean_return=ret_sum / c if c else float("nan"),
                             mean_length=len_sum / c if c else float("nan"),
                             env_steps=steps, seconds=time.perf_counter() - t0)
+
+    def _bootstrap_value(self) -> torch.Tensor:
+        """V(last_obs) for GAE: the MFMA policy kernel when fused (batch-independent rows), else torch."""
+        if self._fp is not None:
+            return self._fp.value(self.last_obs, self._last_v, self._act_env)
+        return self.policy.value(self.last_obs)
 
     # ------------------------------------------------------------------------------------
     def train(self, n_epochs: Optional[int] = None, max_minibatches: Optional[int] = None) -> dict:
