@@ -128,6 +128,9 @@ QD_HD float q_atan2(float y, float x) {
   p = fmaf(p, t2, -0.33332598209381104f);
   p = fmaf(p, t2, 0.9999998807907104f);
   float r = p * t;
+  // |y| == |x| != 0: exactly RN(pi/4), as a correctly rounded atan2 gives (the polynomial is 1 ulp
+  // low there, and quat_to_euler's zero-pitch states -- pure roll / yaw -- land on it)
+  r = (mn == mx && mx > 0.0f) ? 0.785398185253143310546875f : r;
   if (ay > ax) r = 1.57079632679489662f - r;
   if (copysignf(1.0f, x) < 0.0f) r = 3.14159265358979324f - r;  // atan2(y, -0) conventions too
   return copysignf(r, y);
