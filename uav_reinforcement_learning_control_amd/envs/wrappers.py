@@ -8,13 +8,36 @@ from .rate_wrapper import RateControlWrapper
 
 
 class RelPosActWrapper:
-    """7-D observation [normalized rel pos (3), previous action (4)] (wrappers.py:13-25)."""
+    """gym.ObservationWrapper-shaped facade of RelPosActWrapper (wrappers.py:13-25): 7-D
+    observation [normalized rel pos (3), previous action (4)].
+
+    The observation is produced by the step kernel's output stage (QuadCfg.wrapper =
+    QUAD_WRAP_RELPOS, k_step_relpos): wrapping rebuilds `env` (a QuadVecEnv or a HoverEnv /
+    TrajectoryFollowEnv facade) with that wrapper kind, so step/reset already return obs7.
+    `observation(obs12)` is the reference's mapping, for callers that apply it themselves."""
 
     def __init__(self, env):
         from ..utils.spaces import Box
-        self.env = env
+        from .hover_env import HoverEnv
+        from .vec_env import QuadVecEnv
+        if isinstance(env, QuadVecEnv):
+            inner = QuadVecEnv(env.num_envs, env=env.env_kind, wrapper="RelPosActWrapper", device=env.device,
+                               seed=env.seed_value, env_id_base=env.env_id_base,
+                               max_episode_steps=env.max_episode_steps, auto_reset=bool(env.cfg.auto_reset))
+        elif isinstance(env, HoverEnv):
+            inner = type(env)(render_mode=env.render_mode, max_episode_steps=env.max_episode_steps,
+                              device=env._vec.device, wrapper="RelPosActWrapper")
+        else:
+            raise TypeError(f"cannot wrap {type(env).__name__}")
+        env.close()
+        self.env = inner
         self.observation_space = Box(-1.0, 1.0, (7,), np.float32)
-        self.action_space = env.action_space
+        self.action_space = inner.action_space
+
+    def __getattr__(self, name):
+        if name == "env":
+            raise AttributeError(name)
+        return getattr(self.env, name)
 
     @property
     def unwrapped(self):
@@ -24,12 +47,13 @@ class RelPosActWrapper:
         return np.concatenate([obs[0:3], self.unwrapped._prev_action]).astype(np.float32)
 
     def reset(self, **kw):
-        o, i = self.env.reset(**kw)
-        return self.observation(o), i
+        return self.env.reset(**kw)
 
-    def step(self, a):
-        o, r, te, tr, i = self.env.step(a)
-        return self.observation(o), r, te, tr, i
+    def step(self, a, *args, **kw):
+        return self.env.step(a, *args, **kw)
+
+    def close(self) -> None:
+        self.env.close()
 
 
 WRAPPER_REGISTRY = {"RelPosActWrapper": RelPosActWrapper,

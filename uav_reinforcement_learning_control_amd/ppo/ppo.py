@@ -404,5 +404,20 @@ class PPO:
         return self
 
     def state_dict(self) -> dict:
+        """What a resumed run needs: policy, optimizer (Adam moments, step counts), the timestep
+        count and the rollout's action-noise counter (so resumed rollouts draw fresh noise)."""
         return {"policy": self.policy.state_dict(), "optimizer": self.opt.state_dict(),
-                "num_timesteps": self.num_timesteps}
+                "num_timesteps": self.num_timesteps, "noise_step": self._t_host}
+
+    def load_state_dict(self, sd: dict) -> None:
+        """Restore state_dict() (parameters are copied in place, so the gradient bucket binding
+        and the fused kernels' pointers stay valid). Envs restart from reset, as SB3's
+        PPO.load + learn(reset_num_timesteps=False) does."""
+        self.policy.load_state_dict(sd["policy"])
+        self.opt.load_state_dict(sd["optimizer"])
+        for st in self.opt.state.values():  # fused Adam keeps its step counters on the device
+            if "step" in st and torch.is_tensor(st["step"]):
+                st["step"] = st["step"].to(device=self.device, dtype=torch.float32)
+        self.num_timesteps = int(sd["num_timesteps"])
+        self._t_host = int(sd.get("noise_step", 0))
+        self._started = False

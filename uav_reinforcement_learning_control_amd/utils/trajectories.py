@@ -54,8 +54,26 @@ def square(spacing: float = 0.5, side_length: float = 1.5, center=None) -> np.nd
     return np.array(pts)
 
 
-TRAJECTORY_GENERATORS = {"eight": figure_eight, "circle": circle, "square": square}
+def generate_figure_eight(spacing: float = 0.5, radius: float = 1.0, center=None) -> list:
+    """The reference's name and return type (utils/trajectories.py:6): a list of [3] arrays."""
+    return list(figure_eight(spacing, radius, center))
+
+
+def generate_circle(spacing: float = 0.5, radius: float = 1.0, center=None) -> list:
+    """utils/trajectories.py:37."""
+    return list(circle(spacing, radius, center))
+
+
+def generate_square(spacing: float = 0.5, side_length: float = 1.5, center=None) -> list:
+    """utils/trajectories.py:53."""
+    return list(square(spacing, side_length, center))
+
+
+# the reference's registry (utils/trajectories.py:76-81): list-returning generators
+TRAJECTORY_GENERATORS = {"eight": generate_figure_eight, "circle": generate_circle, "square": generate_square}
+_ARRAYS = {"eight": figure_eight, "circle": circle, "square": square}
 
 
 def make_trajectory(name: str, spacing: float = 0.5, center: Optional[np.ndarray] = None, **kw) -> np.ndarray:
-    return TRAJECTORY_GENERATORS[name](spacing=spacing, center=center, **kw)
+    """The named waypoint set as one float64 [n, 3] array (what the batched evaluator uploads)."""
+    return _ARRAYS[name](spacing=spacing, center=center, **kw)
