@@ -32,6 +32,36 @@
 
 #define QD_HD __host__ __device__ __forceinline__
 
+// QD_PROBE (tools/probe/ builds only, never the product): per-wave s_memtime stamps at phase
+// boundaries of the step, to see where a lone wave's time goes. QD_STAMP(st, k) records stamp k
+// into the wave-uniform array st (nullptr: no-op); the scheduling barriers keep instructions from
+// moving across the boundary, so the probe build is slower than the product and only its
+// phase proportions are meaningful.
+#if defined(QD_PROBE) && defined(__HIP_DEVICE_COMPILE__)
+#define QD_STAMP(st, k)                                   \
+  do {                                                    \
+    if (st) {                                             \
+      __builtin_amdgcn_sched_barrier(0);                  \
+      (st)[k] = __builtin_amdgcn_s_memtime();             \
+      __builtin_amdgcn_sched_barrier(0);                  \
+    }                                                     \
+  } while (0)
+// QD_PIN(x): the probe's stamps must not be crossed by IR-level code motion either; an empty
+// volatile asm that reads x forces x to be computed before the next stamp.
+#define QD_PIN(x) asm volatile("" ::"v"(x))
+#else
+#define QD_STAMP(st, k) \
+  do {                  \
+  } while (0)
+#define QD_PIN(x) \
+  do {            \
+  } while (0)
+#endif
+#define QD_PIN_N(arr, n)                                  \
+  do {                                                    \
+    _Pragma("unroll") for (int pin_i_ = 0; pin_i_ < (n); pin_i_++) QD_PIN((arr)[pin_i_]); \
+  } while (0)
+
 namespace quadenv {
 
 // ---------------------------------------------------------------------------------------------
@@ -430,17 +460,25 @@ QD_HD void normalize4(T q[4]) {
   }
 }
 
+template <typename T, bool CHECKS, bool F_NONNEG>
+QD_HD void physics_body(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4], bool bad);
+
 // mujoco.mj_step for one env. Fin: ctrl in float64 (may be NaN / out of range; MuJoCo semantics).
 // CHECKS = false: mjx.step semantics (the brax kinds): no bad-state / bad-ctrl / bad-acc resets,
 // NaN propagates.
 // F_NONNEG: the caller guarantees Fin >= 0 (or -0, or NaN) -- env_step's F * vs -- so the
 // ctrlrange clamp's lower bound (drone.xml's fixed 0, quad_model.h) cannot bind and is skipped.
+// (A speculative form -- step first, screen the loaded state afterwards -- measured slower.)
 template <typename T, bool CHECKS = true, bool F_NONNEG = false>
 QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4]) {
   // mj_checkPos / mj_checkVel: bad state => mj_resetData (qpos0, zero qvel, zero ctrl)
   const T st[21] = {e.pos[0], e.pos[1], e.pos[2], e.q[0], e.q[1], e.q[2], e.q[3], e.th[0], e.th[1], e.th[2], e.th[3],
                     e.v[0], e.v[1], e.v[2], e.w[0], e.w[1], e.w[2], e.s[0], e.s[1], e.s[2], e.s[3]};
-  bool bad = any_bad(st);
+  physics_body<T, CHECKS, F_NONNEG>(c, e, Fin, CHECKS ? any_bad(st) : false);
+}
+
+template <typename T, bool CHECKS, bool F_NONNEG>
+QD_HD void physics_body(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4], bool bad) {
   bool badctrl = false;
 #pragma unroll
   for (int i = 0; i < 4; i++) badctrl |= isbad(Fin[i]);
@@ -637,7 +675,8 @@ QD_HD bool terminated_of(const KConsts<T>& k, const float s12[12]) {
 // (RateControlWrapper.action ->) HoverEnv.step for one env. The control path (CTBR, mixer,
 // voltage sag) runs in float64 like the reference; the rigid-body dynamics in T.
 template <typename T, bool CTBR>
-QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], StepRes& r) {
+QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], StepRes& r,
+                    uint64_t* stamps = nullptr) {
   float a[4];
   a[0] = act[0];
   if (CTBR) {
@@ -674,6 +713,8 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
   const double load = ((F[0] + F[1] + F[2] + F[3]) * 0.25) * k.r_mx;
   const double dV = (k.vb + k.vl * load) * k.dt;
   e.volt = T(clipn(double(e.volt) - dV, k.vmin, k.vnom));
+  if (stamps) { QD_PIN_N(F, 4); QD_PIN(e.volt); }
+  QD_STAMP(stamps, 2);
   // QD_ABL_*: cost-ablation builds of tools/step_variants.py only (never defined in the product)
 #if defined(QD_ABL_PHYS2)
   physics_step<T, true, true>(k.ph, e, F);
@@ -682,6 +723,8 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
   physics_step<T, true, true>(k.ph, e, F);  // F = clip(., 0, max) * vs >= 0 (or NaN)
 #endif
   e.step += 1;
+  if (stamps) { QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.th, 4); QD_PIN_N(e.v, 3); QD_PIN_N(e.w, 3); QD_PIN_N(e.s, 4); }
+  QD_STAMP(stamps, 3);
 #if defined(QD_ABL_NOOBS)
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -693,12 +736,15 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
 #else
   observe(k, e, r.obs, r.state12);
 #endif
+  if (stamps) { QD_PIN_N(r.obs, 12); QD_PIN_N(r.state12, 12); }
+  QD_STAMP(stamps, 4);
   r.reward = reward_of<T>(r.state12, e.target);
   r.term = terminated_of(k, r.state12);
   r.trunc = e.step >= k.max_steps;
 #pragma unroll
   for (int i = 0; i < 4; i++) r.motor[i] = float(F[i]);
   r.vscale = float(vs);
+  if (stamps) { QD_PIN(r.reward); QD_PIN(uint32_t(r.term)); QD_PIN(uint32_t(r.trunc)); QD_PIN_N(r.motor, 4); }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -176,6 +176,15 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
   const bool live = block_first + int(threadIdx.x) < end;
   const int i = live ? block_first + int(threadIdx.x) : end - 1;
   float obs[12];
+#if defined(QD_PROBE)
+  uint64_t stamp_buf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t* stamps = out.target_info ? stamp_buf : nullptr;  // probe builds: target_info = stamp buffer
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+  bool rs_probe = false;
+#else
+  uint64_t* stamps = nullptr;
+#endif
+  QD_STAMP(stamps, 0);
   {
     EnvRegs<float> e;
     load_env(p, i, e, CTBR);
@@ -184,11 +193,23 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
     const uint32_t ep = S.ldu(F_EP, vo);
     const float4 a4 = act[i];
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+#if defined(QD_PROBE)
+    if (stamps) {  // stamp 1: every load of the step has landed
+      settle(ep); settle(__builtin_bit_cast(uint32_t, a4.x)); settle(__builtin_bit_cast(uint32_t, e.volt));
+      settle(__builtin_bit_cast(uint32_t, e.s[3])); settle(uint32_t(e.step)); settle(__builtin_bit_cast(uint32_t, e.target[2]));
+    }
+#endif
+    QD_STAMP(stamps, 1);
     StepRes r;
-    env_step<float, CTBR>(*p.kc, e, a, r);
+    env_step<float, CTBR>(*p.kc, e, a, r, stamps);
+    QD_STAMP(stamps, 5);
     settle(ep);
     const uint32_t o = uint32_t(i) * 4u;
+#if defined(QD_PROBE)
+    if (live && !stamps) {
+#else
     if (live) {
+#endif
       sto(out.reward, o, r.reward);
       sto(out.terminated, uint32_t(i), uint8_t(r.term));
       sto(out.truncated, uint32_t(i), uint8_t(r.trunc));
@@ -210,18 +231,40 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
 #else
     const bool rs = live && (r.term || r.trunc) && p.auto_reset;
 #endif
+#if defined(QD_PROBE)
+    rs_probe = rs;
+#endif
     float u16[16];
     reset_words_wave(p, rl, uint32_t(i), ep, rs, u16);
+    if (stamps && rs) QD_PIN_N(u16, 16);
+    QD_STAMP(stamps, 8);
     if (rs) {
       if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
+      QD_STAMP(stamps, 9);
       float init12[12], tgt[3], s12[12];
       reset_affine_u(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, u16, init12, tgt);
       env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
+      if (stamps) { QD_PIN_N(obs, 12); QD_PIN_N(e.q, 4); }
+      QD_STAMP(stamps, 10);
       S.stu(F_EP, vo, ep + 1u);
     }
+    if (stamps) { QD_PIN_N(obs, 12); QD_PIN_N(e.q, 4); QD_PIN_N(e.pos, 3); }
+    QD_STAMP(stamps, 6);
     if (live) store_env(p, i, e, CTBR);
   }
   store_obs_rows(lds, obs, out.obs, block_first, p.first + p.count);
+#if defined(QD_PROBE)
+  QD_STAMP(stamps, 7);
+  if (stamps && (threadIdx.x & 63) == 0) {
+    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+    uint64_t* dst = reinterpret_cast<uint64_t*>(out.target_info) + size_t(block_first + int(threadIdx.x)) / 64 * 16;
+#pragma unroll
+    for (int k = 0; k < 12; k++) dst[k] = stamp_buf[k];
+    dst[12] = rt0; dst[13] = rt1;
+    dst[14] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID (id 20)
+    dst[15] = __popcll(__ballot(rs_probe));
+  }
+#endif
 }
 
 
