@@ -146,6 +146,8 @@ def _run_rank(args, rank, world, local_rank):
     if rank == 0 and not args.no_configs:
         res["configs"] = {
             "config2_hover_4096": _kernel_rate(4096, "hover", None, dev, args.seed),
+            "config2_hover_4096_one_launch": _kstep_rate(4096, 1000, dev, args.seed),
+            "hover_65536_one_launch_random": _kstep_rate(65536, 200, dev, args.seed),
             "config5_traj_ctbr_65536": _kernel_rate(65536, "trajectory", "RateControlWrapper", dev, args.seed),
             "hover_ctbr_65536": _kernel_rate(65536, "hover", "RateControlWrapper", dev, args.seed)}
     if rank == 0 and args.large_envs > 0:
@@ -176,6 +178,29 @@ def _kernel_rate(n, kind, wrapper, dev, seed) -> dict:
     bpe = BYTES_PER_ENV_STEP + (24 if wrapper else 0)
     return {"envs": n, "env": kind, "wrapper": wrapper, "kernel_us": us,
             "env_steps_per_s": n / (us * 1e-6), "achieved_GBs": bpe * n / (us * 1e-6) / 1e9}
+
+
+def _kstep_rate(n, steps, dev, seed) -> dict:
+    """SURVEY config 2 as one launch (quad_step_random): `steps` random-action steps with state kept
+    on chip, actions drawn in-kernel from quad_random_actions' map; HIP events on the launch's
+    stream after one untimed launch. Per step the same outputs go to HBM as with quad_step."""
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    e = QuadVecEnv(n, env="hover", device=dev, seed=seed)
+    e.reset()
+    e.step_random(50, step0=0)  # warm-up (not timed)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    r = e.step_random(steps, step0=50)
+    e1.record()
+    torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / steps
+    resets = float((r["terminated"] | r["truncated"]).float().mean())
+    del r
+    e.close()
+    return {"envs": n, "steps_per_launch": steps, "kernel": "k_step_random<HOVER,noCTBR>",
+            "us_per_step": us, "env_steps_per_s": n / (us * 1e-6), "reset_fraction_per_step": resets,
+            "bytes_per_env_step_out": 70, "note": "state read/written once per launch; actions drawn in-kernel"}
 
 
 def _end_to_end(env, args, world: int = 1) -> dict:

@@ -166,6 +166,17 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
  * state12 (device [N,12] or NULL): the absolute QuadState vector (HoverEnv._state.vec()). */
 int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream);
 
+/* Config 2 of the scope table -- the random-action rollout of debug_training.py:111
+ * (env.step(env.action_space.sample()) in a loop) -- as ONE launch: `steps` consecutive quad_step
+ * calls with the actions quad_random_actions(step0 + s) gives, the env state kept on chip between
+ * steps. Results are identical to quad_random_actions + quad_step, step by step. Every QuadStepOut
+ * pointer is time-major: obs [steps][N,12], reward / terminated / truncated [steps][N], terminal_obs
+ * [steps][N,12] (optional; rows of envs that finished that step); motor_commands, voltage_scale,
+ * state12 and target_info must be NULL. actions_out: [steps][N,4] (16-byte aligned) or NULL.
+ * Hover / trajectory kinds, wrapper NONE or CTBR; steps * N * 48 < 2^32. */
+int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadStepOut* out, float* actions_out,
+                     void* stream);
+
 /* HoverEnv._is_terminated (hover_env.py:150-157; TrajectoryFollowEnv's bounds for that kind) on n
  * caller-given absolute 12-D states (device [n,12], the QuadState vector: pos, roll/pitch/yaw, world
  * velocity, body rates): terminated[i] = any non-finite component or any component outside the

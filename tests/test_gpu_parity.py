@@ -569,3 +569,58 @@ def test_invalid_arguments_fail_cleanly():
     assert b"aligned" in L.quad_last_error()
     assert L.quad_step(env._h, C.c_void_p(a.data_ptr()), C.byref(out), s) == N.QUAD_OK
     env.close()
+
+
+@pytest.mark.parametrize("env_name,wrapper", [("hover", None), ("trajectory", "RateControlWrapper")])
+def test_step_random_is_the_step_by_step_rollout(env_name, wrapper):
+    """quad_step_random (config 2 in one launch, state on chip) == random_actions + quad_step
+    step by step, bit for bit: every step's obs, reward, flags, terminal obs, the actions, and the
+    final state (incl. episode counters after the auto-resets it crossed)."""
+    n, T = 5000, 40
+    a = _env(n, env_name, wrapper, seed=21, env_id_base=77, max_episode_steps=13)
+    b = _env(n, env_name, wrapper, seed=21, env_id_base=77, max_episode_steps=13)
+    a.reset(); b.reset()
+    res = a.step_random(T, step0=5, actions=True)
+    resets = 0
+    for t in range(T):
+        acts = b.random_actions(5 + t)
+        obs, rew, te, tr, inf = b.step(acts)
+        done = te | tr
+        resets += int(done.sum())
+        assert torch.equal(res["actions"][t], acts), t
+        assert torch.equal(res["obs"][t], obs) and torch.equal(res["reward"][t], rew), t
+        assert torch.equal(res["terminated"][t], te) and torch.equal(res["truncated"][t], tr), t
+        assert torch.equal(res["terminal_observation"][t][done], inf["terminal_observation"][done]), t
+    assert resets > n  # truncation at 13 steps: every env reset at least twice
+    ga, gb = a.get_state(), b.get_state()
+    for k in ga:
+        assert np.array_equal(ga[k], gb[k]), k
+    a.close(); b.close()
+
+
+def test_step_random_against_oracle_short_horizon():
+    """The K-step launch against the float64 oracle from the same start states: every step's obs
+    within the parity bar for 3 steps (one-step errors compound after that), and the reset obs of
+    any env that finishes bit-exact with the oracle's draw of that episode."""
+    n, T = 512, 3
+    env = _env(n, "hover", seed=8, max_episode_steps=2)
+    env.reset()
+    st = env.get_state()
+    res = env.step_random(T, step0=0)
+    cfg = O.default_cfg(O.ENV_HOVER, O.WRAP_NONE)
+    cfg.max_episode_steps = 2
+    obs = res["obs"].cpu().numpy(); te = res["terminated"].cpu().numpy(); tr = res["truncated"].cpu().numpy()
+    for i in range(0, n, 5):
+        e = O.Env(cfg=cfg)
+        e.set_full_state(st["qpos"][i], st["qvel"][i], st["voltage"][i], st["target"][i], st["step_count"][i])
+        ep = st["episode"][i]
+        for t in range(T):
+            o = O.out_to_dict(e.step(O.random_action(8, i, t)))
+            assert o["terminated"] == te[t, i] and o["truncated"] == tr[t, i], (i, t)
+            if o["terminated"] or o["truncated"]:
+                i12, t3 = O.reset_draw(cfg, 8, i, ep)
+                ep += 1
+                assert np.array_equal(obs[t, i], e.reset_with(i12, t3)), (i, t)
+            else:
+                assert parity_ok(obs[t, i], o["obs"]).all(), (i, t, obs[t, i], o["obs"])
+    env.close()

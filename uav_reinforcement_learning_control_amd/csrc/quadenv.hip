@@ -268,6 +268,65 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
 }
 
 
+// Config 2 of the scope table -- debug_training.py:111's loop env.step(env.action_space.sample())
+// -- as ONE launch: `steps` whole k_step steps per thread with the action of step s drawn in-kernel
+// from quad_random_actions' map, Philox(seed; gid, step0 + s, 0x100), and the env state kept in
+// registers between steps (read once, written once). Per step every output row goes to HBM as in
+// k_step: obs [N,12] through the block's LDS transpose, reward, flags, terminal obs of finishing
+// envs, all time-major [steps][N, ...]. Same env_step code as k_step, so the same bits.
+template <int KIND, bool CTBR>
+__global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __restrict__ kc, KParams p,
+                                                       QuadStepOut out, float4* __restrict__ act_out,
+                                                       uint32_t step0, int32_t steps) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
+  __shared__ float4 lds[BLOCK * 3];
+  __shared__ ResetLds rl;
+  const int block_first = blockIdx.x * BLOCK;
+  const int n = p.n;
+  const bool live = block_first + int(threadIdx.x) < n;
+  const int i = live ? block_first + int(threadIdx.x) : n - 1;  // shadow lanes: in-range, store nothing
+  EnvRegs<float> e;
+  load_env(p, i, e, CTBR);
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
+  uint32_t ep = S.ldu(F_EP, vo);
+  const uint64_t gid = p.gid_base + uint64_t(i);
+  for (int t = 0; t < steps; t++) {
+    uint32_t c[4] = {uint32_t(gid), uint32_t(gid >> 32), step0 + uint32_t(t), 0x100u};
+    philox4x32_10(c, uint32_t(p.seed), uint32_t(p.seed >> 32));
+    const float a[4] = {float(c[0] >> 8) * 0x1p-23f - 1.0f, float(c[1] >> 8) * 0x1p-23f - 1.0f,
+                        float(c[2] >> 8) * 0x1p-23f - 1.0f, float(c[3] >> 8) * 0x1p-23f - 1.0f};
+    StepRes r;
+    env_step<float, CTBR>(*p.kc, e, a, r);
+    const uint32_t row = uint32_t(t) * uint32_t(n) + uint32_t(i);  // time-major row (< 2^32: checked)
+    if (live) {
+      sto(out.reward, 4u * row, r.reward);
+      sto(out.terminated, row, uint8_t(r.term));
+      sto(out.truncated, row, uint8_t(r.trunc));
+      if (act_out) sto(act_out, 16u * row, make_float4(a[0], a[1], a[2], a[3]));
+    }
+    float obs[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
+    const bool rs = live && (r.term || r.trunc) && p.auto_reset;
+    float u16[16];
+    reset_words_wave(p, rl, uint32_t(i), ep, rs, u16);
+    if (rs) {
+      if (out.terminal_obs) store_row12(out.terminal_obs, row, r.obs);
+      float init12[12], tgt[3], s12[12];
+      reset_affine_u(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, u16, init12, tgt);
+      env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
+      ep += 1u;
+    }
+    store_obs_rows(lds, obs, out.obs + size_t(t) * size_t(n) * 12, block_first, n);
+    __syncthreads();  // the next step reuses the LDS rows
+  }
+  if (live) {
+    store_env(p, i, e, CTBR);
+    S.stu(F_EP, vo, ep);
+  }
+}
+
 // RelPosActWrapper (envs/wrappers.py:13-25) around HoverEnv / TrajectoryFollowEnv: the same step,
 // emitting obs7 = [obs[0:3], _prev_action] where _prev_action is the action just taken
 // (hover_env.py:166) and zeros after a reset (:212). The previous action is kept in the SoA
@@ -1364,6 +1423,39 @@ int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream) {
   else
     hipLaunchKernelGGL(k_observe<false>, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
                        h->kp, obs, state12);
+  HIP_TRY(hipGetLastError());
+  return QUAD_OK;
+}
+
+int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadStepOut* out, float* actions_out,
+                     void* stream) {
+  if (!h || !out) return fail(QUAD_EINVAL, "handle/out is NULL");
+  if (steps < 0) return fail(QUAD_EINVAL, "steps must be >= 0");
+  if (steps == 0) return QUAD_OK;
+  if (h->cfg.env_kind != QUAD_ENV_HOVER && h->cfg.env_kind != QUAD_ENV_TRAJ)
+    return fail(QUAD_EINVAL, "quad_step_random drives the hover / trajectory kinds");
+  if (h->cfg.wrapper == QUAD_WRAP_RELPOS) return fail(QUAD_EINVAL, "quad_step_random: wrapper NONE or CTBR");
+  if (!out->obs || !out->reward || !out->terminated || !out->truncated)
+    return fail(QUAD_EINVAL, "obs, reward, terminated and truncated are required");
+  if (out->motor_commands || out->voltage_scale || out->state12 || out->target_info)
+    return fail(QUAD_EINVAL, "quad_step_random writes obs, reward, flags and terminal_obs only");
+  if ((reinterpret_cast<uintptr_t>(out->obs) | reinterpret_cast<uintptr_t>(actions_out)) & 15u)
+    return fail(QUAD_EINVAL, "obs and actions_out must be 16-byte aligned");
+  if (int64_t(steps) * h->n * 48 > int64_t(UINT32_MAX))
+    return fail(QUAD_EINVAL, "steps * N too large for one launch (time-major rows use 32-bit byte offsets)");
+  DeviceGuard g(h->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(grid_of(h->n)), blk(BLOCK);
+  float4* ao = reinterpret_cast<float4*>(actions_out);
+  const bool traj = h->cfg.env_kind == QUAD_ENV_TRAJ, ctbr = h->cfg.wrapper == QUAD_WRAP_CTBR;
+  if (traj && ctbr)
+    hipLaunchKernelGGL((k_step_random<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
+  else if (traj)
+    hipLaunchKernelGGL((k_step_random<QUAD_ENV_TRAJ, false>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
+  else if (ctbr)
+    hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, true>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
+  else
+    hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, false>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
 }

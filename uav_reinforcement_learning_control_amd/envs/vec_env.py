@@ -196,6 +196,30 @@ class QuadVecEnv:
                 "quad_terminated")
         return out
 
+    def step_random(self, steps: int, step0: int = 0, terminal_obs: bool = True, actions: bool = False) -> dict:
+        """`steps` consecutive steps with action_space.sample()-style actions (the map of
+        random_actions(step0 + s)) in ONE launch (quad_step_random, SURVEY config 2): returns
+        time-major tensors obs [steps, N, 12], reward, terminated, truncated [steps, N], and
+        terminal_observation [steps, N, 12] (rows of envs that finished) / actions [steps, N, 4]
+        when asked. Identical to calling random_actions + step `steps` times."""
+        if self.brax or self.obs_dim != 12:
+            raise ValueError("step_random drives the hover / trajectory kinds (12-D obs)")
+        n, dev, T = self.num_envs, self.device, int(steps)
+        res = {"obs": torch.empty(T, n, 12, dtype=torch.float32, device=dev),
+               "reward": torch.empty(T, n, dtype=torch.float32, device=dev),
+               "terminated": torch.empty(T, n, dtype=torch.bool, device=dev),
+               "truncated": torch.empty(T, n, dtype=torch.bool, device=dev)}
+        if terminal_obs:
+            res["terminal_observation"] = torch.zeros(T, n, 12, dtype=torch.float32, device=dev)
+        if actions:
+            res["actions"] = torch.empty(T, n, 4, dtype=torch.float32, device=dev)
+        out = N.QuadStepOut(obs=res["obs"].data_ptr(), reward=res["reward"].data_ptr(),
+                            terminated=res["terminated"].data_ptr(), truncated=res["truncated"].data_ptr(),
+                            terminal_obs=_ptr(res.get("terminal_observation")))
+        N.check(N.lib().quad_step_random(self._h, int(step0) & 0xFFFFFFFF, T, C.byref(out),
+                                         _ptr(res.get("actions")), self._stream()), "quad_step_random")
+        return res
+
     def random_actions(self, step_index: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """action_space.sample() for every env (Philox(seed, env id, step_index))."""
         out = torch.empty(self.num_envs, 4, dtype=torch.float32, device=self.device) \
