@@ -156,8 +156,11 @@ def _run_rank(args, rank, world, local_rank):
         torch.cuda.empty_cache()
         big = QuadVecEnv(args.large_envs, env="hover", device=dev, seed=args.seed)
         big.reset()
-        acts = [big.random_actions(k) for k in range(4)]
-        res["large_kernel_us"] = _gated_kernel_us(_quad_step_fn(big), acts, 200)
+        acts = [big.random_actions(k) for k in range(8)]
+        st = _quad_step_fn(big)
+        for k in range(50):  # past the post-reset transient: ~11 % of envs reset per step from here on
+            st(acts[k % 8].data_ptr())
+        res["large_kernel_us"] = _gated_kernel_us(st, acts, 200)
         big.close()
     else:
         env.close()

@@ -109,8 +109,32 @@ def kernel_variant(request, monkeypatch):
     return request.param
 
 
+@pytest.fixture(params=["1", "0"])
+def spec_mode(request, monkeypatch):
+    """Default-config handles run the kernels with the reference constants compiled in
+    (kconsts_default.h); QUADENV_SPEC=0 forces the generic kernels that read the handle's block."""
+    monkeypatch.setenv("QUADENV_SPEC", request.param)
+    return request.param
+
+
+def test_kernel_form_selection(spec_mode):
+    from uav_reinforcement_learning_control_amd import _native as N
+    for n, lanes in ((4096, 0), (65536, 0), (300000, 1)):
+        e = _env(n)
+        assert N.lib().quad_kernel_form(e._h) == lanes | (16 if spec_mode == "1" else 0), n
+        e.close()
+    for kw in (dict(max_episode_steps=100), dict(cfg_overrides=dict(density=1.0))):
+        e = _env(1024, **kw)  # not the reference default: generic kernels
+        assert N.lib().quad_kernel_form(e._h) == 0
+        e.close()
+    for env_name, wrapper in (("hover", "RateControlWrapper"), ("trajectory", None), ("trajectory", "RateControlWrapper")):
+        e = _env(1024, env_name, wrapper)
+        assert N.lib().quad_kernel_form(e._h) == (16 if spec_mode == "1" else 0), (env_name, wrapper)
+        e.close()
+
+
 @pytest.mark.parametrize("env_name,wrapper,kind,wrap", VARIANTS)
-def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap, kernel_variant):
+def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap, kernel_variant, spec_mode):
     n = 3000
     rng = np.random.default_rng(17 + kind * 2 + wrap)
     st = _random_states(n, rng)
@@ -138,7 +162,7 @@ def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap, kernel
     nv, ov = operand_only(g["qvel"], np.stack([o["qvel"] for o in ref]), st["qvel"])
     ns, os_ = operand_only(g["state12"], np.stack([o["state12"] for o in ref]),
                            np.stack([_pre12(st, i) for i in range(n)]))
-    print(f"\noperand-relative-only components ({env_name}, {wrapper}, lanes {kernel_variant}): "
+    print(f"\noperand-relative-only components ({env_name}, {wrapper}, lanes {kernel_variant}, spec {spec_mode}): "
           f"qpos {nq}, qvel {nv}, state12 {ns} of {n} envs")
     assert len(oq) == len(ov) == len(os_) == 0, (oq[:5], ov[:5], os_[:5])
     assert nq + nv + ns <= 0.01 * n
@@ -148,7 +172,7 @@ def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap, kernel
 @pytest.mark.parametrize("name,kind,wrap,ms", [("hover_steps", 0, 0, None), ("hover_trunc", 0, 0, 15),
                                                ("hover_nan", 0, 0, None), ("ctbr_steps", 0, 1, None),
                                                ("traj_ctbr_steps", 1, 1, None), ("traj_steps", 1, 0, None)])
-def test_step_matches_reference_goldens(golden_dir, name, kind, wrap, ms, kernel_variant):
+def test_step_matches_reference_goldens(golden_dir, name, kind, wrap, ms, kernel_variant, spec_mode):
     d = np.load(os.path.join(golden_dir, f"golden_{name}.npz"))
     n = len(d["action"])
     env = _env(n, "trajectory" if kind else "hover", "RateControlWrapper" if wrap else None,
@@ -572,13 +596,14 @@ def test_invalid_arguments_fail_cleanly():
 
 
 @pytest.mark.parametrize("env_name,wrapper", [("hover", None), ("trajectory", "RateControlWrapper")])
-def test_step_random_is_the_step_by_step_rollout(env_name, wrapper):
+def test_step_random_is_the_step_by_step_rollout(env_name, wrapper, spec_mode):
     """quad_step_random (config 2 in one launch, state on chip) == random_actions + quad_step
     step by step, bit for bit: every step's obs, reward, flags, terminal obs, the actions, and the
     final state (incl. episode counters after the auto-resets it crossed)."""
     n, T = 5000, 40
-    a = _env(n, env_name, wrapper, seed=21, env_id_base=77, max_episode_steps=13)
-    b = _env(n, env_name, wrapper, seed=21, env_id_base=77, max_episode_steps=13)
+    ms = 13 if spec_mode == "0" else None  # the default episode length keeps the SPEC kernels
+    a = _env(n, env_name, wrapper, seed=21, env_id_base=77, max_episode_steps=ms)
+    b = _env(n, env_name, wrapper, seed=21, env_id_base=77, max_episode_steps=ms)
     a.reset(); b.reset()
     res = a.step_random(T, step0=5, actions=True)
     resets = 0
@@ -591,7 +616,7 @@ def test_step_random_is_the_step_by_step_rollout(env_name, wrapper):
         assert torch.equal(res["obs"][t], obs) and torch.equal(res["reward"][t], rew), t
         assert torch.equal(res["terminated"][t], te) and torch.equal(res["truncated"][t], tr), t
         assert torch.equal(res["terminal_observation"][t][done], inf["terminal_observation"][done]), t
-    assert resets > n  # truncation at 13 steps: every env reset at least twice
+    assert resets > (n if ms else n // 10)  # (13-step episodes: every env resets at least twice)
     ga, gb = a.get_state(), b.get_state()
     for k in ga:
         assert np.array_equal(ga[k], gb[k]), k

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Summarize tools/pmc/issue_roofline.sh into profiles/<round>/pmc_issue.json and
+profiles/pmc_issue.json (bench.py reads the latter into roofline.issue).
+
+Per step-kernel dispatch (median over dispatches 20..end, past the post-reset transient):
+  instructions per wave by class (SQ_INSTS_*), i.e. per 64 env-steps (one env per lane);
+  the lone-wave issue floor: a wave issues at most one vector instruction per 4 cycles
+  (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so one wave per SIMD needs
+  >= 4 * (VALU + VMEM + LDS) cycles + SALU/SMEM/branch slots;
+  wave cycles and their split (SQ_WAVE_CYCLES = WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY,
+  quad-cycles), VALU-active share, and the effective clock GRBM_GUI_ACTIVE / 8 / kernel time."""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+
+def load(root):
+    d = defaultdict(lambda: defaultdict(list))  # (kernel, grid) -> counter -> [values in dispatch order]
+    for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True)):
+        rows = list(csv.DictReader(open(f)))
+        rows.sort(key=lambda r: int(r.get("Dispatch_Id", r.get("Correlation_Id", 0)) or 0))
+        for r in rows:
+            grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
+            d[(r["Kernel_Name"].split("(")[0], grid)][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return d
+
+
+def trace_us(root):
+    out = {}
+    for f in glob.glob(f"{root}/**/*kernel_trace.csv", recursive=True):
+        rows = list(csv.DictReader(open(f)))
+        ks = [r for r in rows if "k_step" in r["Kernel_Name"]]
+        if ks:
+            du = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in ks[20:]] or \
+                 [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in ks]
+            out[int(ks[0].get("Grid_Size", ks[0].get("Grid_Size_X", 0)))] = statistics.median(du)
+    return out
+
+
+def main(root="gpurun_out/issue", rnd="r02"):
+    res = {}
+    traces = {}
+    for name, n in (("trace", 65536), ("trace1m", 1048576)):
+        t = trace_us(os.path.join(root, name))
+        if t:
+            traces[n] = list(t.values())[0]
+    for n in (65536, 1048576):
+        d = load(os.path.join(root, f"n{n}"))
+        if not d:
+            continue
+        key = max(d, key=lambda k: len(d[k]))
+        c = {k: statistics.median(v[20:] or v) for k, v in d[key].items()}
+        waves = c.get("SQ_WAVES", 0) or 1
+        per_wave = {k[len("SQ_INSTS_"):].lower(): c[k] / waves for k in c if k.startswith("SQ_INSTS_")}
+        vec = per_wave.get("valu", 0) + per_wave.get("vmem_rd", 0) + per_wave.get("vmem_wr", 0) + per_wave.get("lds", 0)
+        sca = per_wave.get("salu", 0) + per_wave.get("smem", 0) + per_wave.get("branch", 0)
+        us = traces.get(n)
+        r = {"kernel": key[0], "grid": key[1], "envs": n, "waves": waves,
+             "instructions_per_wave": per_wave, "vector_instructions_per_wave": vec,
+             "scalar_instructions_per_wave": sca, "kernel_us_rocprof_trace": us}
+        if "SQ_WAVE_CYCLES" in c:
+            wc = c["SQ_WAVE_CYCLES"] * 4 / waves  # quad-cycles -> cycles, per wave
+            r["wave_cycles"] = wc
+            for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
+                      "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_MISC"):
+                if k in c:
+                    r[k.lower() + "_share"] = c[k] * 4 / waves / wc
+            # lone-wave issue floor vs the measured wave lifetime (same counters, same dispatches)
+            r["issue_floor_cycles"] = 4 * vec + sca
+            r["frac_issue_floor"] = r["issue_floor_cycles"] / wc
+        if us and "GRBM_GUI_ACTIVE" in c:
+            r["effective_clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3)
+        res[str(n)] = r
+    for d in (os.path.join("profiles", rnd), "profiles"):
+        os.makedirs(d, exist_ok=True)
+        json.dump(res, open(os.path.join(d, "pmc_issue.json"), "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])

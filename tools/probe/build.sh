@@ -7,6 +7,6 @@ make -s
 mkdir -p ../../tools/_build/obj
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on -fno-slp-vectorize"
 O=../_lib/obj
-/opt/rocm/bin/hipcc $F -DQD_PROBE ${EXTRA:-} -c -o ../../tools/_build/obj/quadenv_probe.o quadenv.hip
+/opt/rocm/bin/hipcc $F -I$O -DQD_PROBE ${EXTRA:-} -c -o ../../tools/_build/obj/quadenv_probe.o quadenv.hip
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_build/probe.so \
   ../../tools/_build/obj/quadenv_probe.o $O/policy.o $O/rollout.o $O/learner.o

@@ -10,12 +10,12 @@ mkdir -p ../../tools/_build/obj
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on"
 O=../_lib/obj
 for v in PHYS2 NOPHYS NOOBS NORESET; do
-  ( /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DQD_ABL_$v -c -o ../../tools/_build/obj/quadenv_$v.o quadenv.hip &&
+  ( /opt/rocm/bin/hipcc $F -I$O -fno-slp-vectorize -DQD_ABL_$v -c -o ../../tools/_build/obj/quadenv_$v.o quadenv.hip &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_build/abl_$v.so \
       ../../tools/_build/obj/quadenv_$v.o $O/policy.o $O/rollout.o $O/learner.o ) &
 done
 # the product source WITH the SLP vectorizer (v_pk_* f32 packing; csrc/Makefile turns it off)
-( /opt/rocm/bin/hipcc $F -c -o ../../tools/_build/obj/quadenv_SLP.o quadenv.hip &&
+( /opt/rocm/bin/hipcc $F -I$O -c -o ../../tools/_build/obj/quadenv_SLP.o quadenv.hip &&
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_build/abl_SLP.so \
     ../../tools/_build/obj/quadenv_SLP.o $O/policy.o $O/rollout.o $O/learner.o ) &
 wait

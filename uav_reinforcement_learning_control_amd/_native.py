@@ -93,7 +93,7 @@ class QuadPolicyAct(C.Structure):
 # every symbol include/quadenv.h declares (checked by tests/test_abi.py)
 EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_create",
            "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe", "quad_terminated", "quad_step_random",
-           "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
+           "quad_kernel_form", "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
            "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
            "quad_waypoints_begin", "quad_waypoints_update", "quad_ppo_workspace_bytes", "quad_ppo_grad",
            "quad_adam_workspace_bytes", "quad_clip_adam")
@@ -152,6 +152,8 @@ def _declare(L):
     L.quad_observe.argtypes = [vp, vp, vp, vp]
     L.quad_terminated.argtypes = [vp, vp, i32, vp, vp]
     L.quad_step_random.argtypes = [vp, u32, i32, C.POINTER(QuadStepOut), vp, vp]
+    L.quad_kernel_form.argtypes = [vp]
+    L.quad_kernel_form.restype = i32
     L.quad_random_actions.argtypes = [vp, u32, vp, vp]
     L.quad_get_state.argtypes = [vp, C.POINTER(QuadStateSoA), i32, vp]
     L.quad_set_state.argtypes = [vp, C.POINTER(QuadStateSoA), i32, vp]

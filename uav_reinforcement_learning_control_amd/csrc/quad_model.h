@@ -19,6 +19,78 @@
 
 namespace quadenv {
 
+// The reference defaults for (env_kind, wrapper), arguments already validated (quad_default_cfg in
+// quadenv.hip; also the build-time generator of the specialized constant blocks, gen_kconsts.cpp):
+// HoverEnv.__init__ (hover_env.py:15-100), TrajectoryFollowEnv.__init__ (trajectory_follow_env.py:
+// 22-104), RateControlWrapper.__init__ (rate_wrapper.py:40-64) with pid_gains.json:43-52,
+// drone_config.py:9-22, drone.xml:4, and the brax kinds' train_brax_ppo.py defaults.
+inline void default_cfg_fill(int32_t env_kind, int32_t wrapper, QuadCfg* c) {
+  std::memset(c, 0, sizeof *c);
+  c->env_kind = env_kind;
+  c->wrapper = wrapper;
+  c->auto_reset = 1;
+  const double pi = M_PI;
+  // HoverEnv._obs_bounds (hover_env.py:36-39) / _state_bounds (:54-57) share the angle/vel rows
+  const double ol[12] = {-4, -4, -2, -pi, -pi, -pi, -10, -10, -10, -6 * pi, -6 * pi, -6 * pi};
+  // _initial_state_bounds (hover_env.py:42-45; trajectory_follow_env.py:49-52)
+  const double il[12] = {-1.5, -1.5, 0.1, -0.3, -0.3, -0.3, -0.5, -0.5, -0.5, -0.5, -0.5, -0.5};
+  const double ih[12] = {1.5, 1.5, 1.5, 0.3, 0.3, 0.3, 0.5, 0.5, 0.5, 0.5, 0.5, 0.5};
+  for (int i = 0; i < 12; i++) {
+    c->obs_low[i] = float(ol[i]);
+    c->obs_high[i] = float(-ol[i]);
+    c->init_low[i] = float(il[i]);
+    c->init_high[i] = float(ih[i]);
+    c->term_low[i] = float(ol[i]);
+    c->term_high[i] = float(-ol[i]);
+  }
+  const double xy = env_kind == QUAD_ENV_TRAJ ? 3.0 : 2.0;  // traj :60-63, hover :54-57
+  c->term_low[0] = float(-xy); c->term_low[1] = float(-xy); c->term_low[2] = 0.f;
+  c->term_high[0] = float(xy); c->term_high[1] = float(xy); c->term_high[2] = float(xy);
+  c->max_episode_steps = env_kind == QUAD_ENV_TRAJ ? 2048 : 512;
+  c->nominal_voltage = env_kind == QUAD_ENV_TRAJ ? 16.8 : 8.4;
+  c->min_voltage = env_kind == QUAD_ENV_TRAJ ? 13.2 : 7.6;
+  const float tl[3] = {-1.5f, -1.5f, 0.3f}, th[3] = {1.5f, 1.5f, 1.8f};  // hover_env.py:48-51
+  for (int i = 0; i < 3; i++) { c->target_low[i] = tl[i]; c->target_high[i] = th[i]; }
+  c->max_motor_thrust = 13.0;  // drone_config.py:9-11,21
+  c->arm_length = 0.039799;
+  c->yaw_coeff = 0.0201;
+  c->max_torque = 0.5;
+  const float al[4] = {0.f, -0.5f, -0.5f, -0.5f}, ah[4] = {52.f, 0.5f, 0.5f, 0.5f};  // :60-65
+  for (int i = 0; i < 4; i++) { c->act_low[i] = al[i]; c->act_high[i] = ah[i]; }
+  c->vdrop_base = 0.01;
+  c->vdrop_load = 0.08;
+  c->rate_max_rad = 360.0 * (M_PI / 180.0);  // rate_wrapper.py:52, pid_gains.json:43-52
+  c->rate_kd[0] = 26; c->rate_kd[1] = 26; c->rate_kd[2] = 18;
+  c->rate_ki = 0.025;
+  c->rate_imax = 0.01;
+  c->inertia[0] = 4.16e-4; c->inertia[1] = 4.23e-4; c->inertia[2] = 5.37e-4;
+  c->timestep = 0.01;  // drone.xml:4
+  c->gravity[2] = -9.81;
+  c->density = 1.225;
+  c->viscosity = 1.8e-5;
+  {  // TrajectoryFollowEnv spline (trajectory_follow_env.py:25, :55-58, :199-203)
+    const float lo[3] = {-1.f, -1.f, 0.4f}, hi[3] = {1.f, 1.f, 1.4f}, amp[3] = {0.6f, 0.6f, 0.4f};
+    for (int i = 0; i < 3; i++) {
+      c->spline_center_low[i] = lo[i]; c->spline_center_high[i] = hi[i]; c->spline_amp[i] = amp[i];
+    }
+    c->spline_duration = 30.f;
+  }
+  if (env_kind >= QUAD_ENV_BRAX_HOVER) {  // train_brax_ppo.py
+    const bool traj = env_kind == QUAD_ENV_BRAX_TRAJ;
+    c->max_episode_steps = 500;                        // --episode-length (:436)
+    for (int i = 0; i < 3; i++) { c->target_low[i] = c->target_high[i] = i == 2 ? 1.f : 0.f; }  // (:55)
+    c->term_low[0] = c->term_low[1] = -3.f; c->term_high[0] = c->term_high[1] = 3.f;  // (:48-50)
+    c->term_low[2] = 0.02f; c->term_high[2] = 4.f;
+    c->reset_noise = 0.01f;                            // (:105-116, :271-272)
+    c->reward_pos_coef = traj ? 1.f : 2.f;             // (:146 / :338)
+    c->reward_action_coef = traj ? 0.001f : 0.f;       // (:339)
+    c->vel_limit = traj ? 20.f : 0.f;                  // (:190)
+    const float cen[3] = {0.f, 0.f, 1.f}, amp[3] = {0.5f, 0.5f, 0.2f}, fr[3] = {0.2f, 0.15f, 0.1f};
+    for (int i = 0; i < 3; i++) { c->traj_center[i] = cen[i]; c->traj_amp[i] = amp[i]; c->traj_freq[i] = fr[i]; }
+    c->traj_duration = 5.f;                            // --traj-duration-seconds (:444)
+  }
+}
+
 struct ModelData {
   // base_link (drone.xml:34-52): free joint, inertial at origin
   double m0 = 0.195;

@@ -27,6 +27,7 @@
 #include "quad_model.h"
 #include "quad_physics.h"
 #include "env_tiles.h"
+#include "kconsts_default.h"
 #include "rollout.h"
 
 using namespace quadenv;
@@ -149,13 +150,13 @@ __device__ __forceinline__ void store_obs_rows(float4* lds, const float obs[12],
 // info["target", "target_vel", "target_acc"] of the step just taken (before any auto-reset);
 // `ep` is the episode counter as loaded (the running episode is ep - 1)
 template <int KIND>
-__device__ __forceinline__ void target_info_of(const KParams& p, int i, const EnvRegs<float>& e,
-                                               uint32_t ep, float o[9]) {
+__device__ __forceinline__ void target_info_of(const KConsts<float>& K, const KParams& p, int i,
+                                               const EnvRegs<float>& e, uint32_t ep, float o[9]) {
   o[0] = e.target[0]; o[1] = e.target[1]; o[2] = e.target[2];
 #pragma unroll
   for (int j = 3; j < 9; j++) o[j] = 0.f;
   if (KIND == QUAD_ENV_TRAJ)  // the target register holds the start position (= traj_pos[0])
-    traj_spline_info(*p.kc, p.seed, p.gid_base + uint64_t(i), ep - 1u, e.target, e.step, o);
+    traj_spline_info(K, p.seed, p.gid_base + uint64_t(i), ep - 1u, e.target, e.step, o);
 }
 
 __device__ __forceinline__ void store_target_info(float* __restrict__ out, int i, const float o[9]) {
@@ -163,12 +164,11 @@ __device__ __forceinline__ void store_target_info(float* __restrict__ out, int i
   for (int j = 0; j < 9; j++) sto(out, uint32_t(i) * 36u + 4u * j, o[j]);
 }
 
+// The step of one env per thread; K is the handle's constant block (k_step's SPEC form passes a
+// compile-time copy of the default block, so every constant is an immediate).
 template <int KIND, bool CTBR>
-__global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict__ kc, KParams p,
-                                                const float4* __restrict__ act, QuadStepOut out) {
-  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores below (see KParams)
-  __shared__ float4 lds[BLOCK * 3];
-  __shared__ ResetLds rl;
+__device__ __forceinline__ void step_body(const KConsts<float>& K, KParams p, const float4* __restrict__ act,
+                                          QuadStepOut out, float4* lds, ResetLds& rl) {
   const int block_first = p.first + blockIdx.x * BLOCK;
   const int end = p.first + p.count;
   // Every thread runs the step: the reset draws are computed by the whole wave (reset_words_wave),
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
 #endif
     QD_STAMP(stamps, 1);
     StepRes r;
-    env_step<float, CTBR>(*p.kc, e, a, r, stamps);
+    env_step<float, CTBR>(K, e, a, r, stamps);
     QD_STAMP(stamps, 5);
     settle(ep);
     const uint32_t o = uint32_t(i) * 4u;
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
       if (out.state12) store_row12(out.state12, uint32_t(i), r.state12);
       if (out.target_info) {
         float info[9];
-        target_info_of<KIND>(p, i, e, ep, info);
+        target_info_of<KIND>(K, p, i, e, ep, info);
         store_target_info(out.target_info, i, info);
       }
     }
@@ -242,8 +242,8 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
       if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
       QD_STAMP(stamps, 9);
       float init12[12], tgt[3], s12[12];
-      reset_affine_u(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, u16, init12, tgt);
-      env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
+      reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
+      env_reset_from<float, KIND>(K, e, init12, tgt, obs, s12);
       if (stamps) { QD_PIN_N(obs, 12); QD_PIN_N(e.q, 4); }
       QD_STAMP(stamps, 10);
       S.stu(F_EP, vo, ep + 1u);
@@ -267,6 +267,23 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
 #endif
 }
 
+// k_step: one env per thread. SPEC: the handle's constant block equals the reference default
+// (quad_create checks the bytes), so the constants are compiled in -- no scalar loads of the block
+// and no waits on them inside the step.
+template <int KIND, bool CTBR, bool SPEC>
+__global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict__ kc, KParams p,
+                                                const float4* __restrict__ act, QuadStepOut out) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores below (see KParams)
+  __shared__ float4 lds[BLOCK * 3];
+  __shared__ ResetLds rl;
+  if constexpr (SPEC) {
+    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
+    step_body<KIND, CTBR>(K, p, act, out, lds, rl);
+  } else {
+    step_body<KIND, CTBR>(*kc, p, act, out, lds, rl);
+  }
+}
+
 
 // Config 2 of the scope table -- debug_training.py:111's loop env.step(env.action_space.sample())
 // -- as ONE launch: `steps` whole k_step steps per thread with the action of step s drawn in-kernel
@@ -275,12 +292,9 @@ __global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict
 // k_step: obs [N,12] through the block's LDS transpose, reward, flags, terminal obs of finishing
 // envs, all time-major [steps][N, ...]. Same env_step code as k_step, so the same bits.
 template <int KIND, bool CTBR>
-__global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __restrict__ kc, KParams p,
-                                                       QuadStepOut out, float4* __restrict__ act_out,
-                                                       uint32_t step0, int32_t steps) {
-  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
-  __shared__ float4 lds[BLOCK * 3];
-  __shared__ ResetLds rl;
+__device__ __forceinline__ void step_random_body(const KConsts<float>& K, KParams p, QuadStepOut out,
+                                                 float4* __restrict__ act_out, uint32_t step0, int32_t steps,
+                                                 float4* lds, ResetLds& rl) {
   const int block_first = blockIdx.x * BLOCK;
   const int n = p.n;
   const bool live = block_first + int(threadIdx.x) < n;
@@ -297,7 +311,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __r
     const float a[4] = {float(c[0] >> 8) * 0x1p-23f - 1.0f, float(c[1] >> 8) * 0x1p-23f - 1.0f,
                         float(c[2] >> 8) * 0x1p-23f - 1.0f, float(c[3] >> 8) * 0x1p-23f - 1.0f};
     StepRes r;
-    env_step<float, CTBR>(*p.kc, e, a, r);
+    env_step<float, CTBR>(K, e, a, r);
     const uint32_t row = uint32_t(t) * uint32_t(n) + uint32_t(i);  // time-major row (< 2^32: checked)
     if (live) {
       sto(out.reward, 4u * row, r.reward);
@@ -314,8 +328,8 @@ __global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __r
     if (rs) {
       if (out.terminal_obs) store_row12(out.terminal_obs, row, r.obs);
       float init12[12], tgt[3], s12[12];
-      reset_affine_u(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, u16, init12, tgt);
-      env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
+      reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
+      env_reset_from<float, KIND>(K, e, init12, tgt, obs, s12);
       ep += 1u;
     }
     store_obs_rows(lds, obs, out.obs + size_t(t) * size_t(n) * 12, block_first, n);
@@ -324,6 +338,21 @@ __global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __r
   if (live) {
     store_env(p, i, e, CTBR);
     S.stu(F_EP, vo, ep);
+  }
+}
+
+template <int KIND, bool CTBR, bool SPEC>
+__global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __restrict__ kc, KParams p,
+                                                       QuadStepOut out, float4* __restrict__ act_out,
+                                                       uint32_t step0, int32_t steps) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
+  __shared__ float4 lds[BLOCK * 3];
+  __shared__ ResetLds rl;
+  if constexpr (SPEC) {
+    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
+    step_random_body<KIND, CTBR>(K, p, out, act_out, step0, steps, lds, rl);
+  } else {
+    step_random_body<KIND, CTBR>(*kc, p, out, act_out, step0, steps, lds, rl);
   }
 }
 
@@ -347,7 +376,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_relpos(const KConsts<float>* __r
   StepRes r;
   env_step<float, false>(*p.kc, e, a, r);
   float info[9];
-  if (out.target_info) target_info_of<KIND>(p, i, e, ep, info);
+  if (out.target_info) target_info_of<KIND>(*p.kc, p, i, e, ep, info);
   float o7[7] = {r.obs[0], r.obs[1], r.obs[2], a[0], a[1], a[2], a[3]};
   float prev[4] = {a[0], a[1], a[2], a[3]};
   const bool rs = (r.term || r.trunc) && p.auto_reset;
@@ -397,9 +426,8 @@ __device__ __forceinline__ T grp_pick(int m, const T* v) {  // v[m], m lane-depe
 }
 
 template <int KIND, bool CTBR, int G>
-__global__ __launch_bounds__(BLOCK) void k_step_g(const KConsts<float>* __restrict__ kc, KParams p,
-                                                  const float4* __restrict__ act, QuadStepOut out) {
-  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
+__device__ __forceinline__ void step_g_body(const KConsts<float>& k, KParams p, const float4* __restrict__ act,
+                                            QuadStepOut out) {
   constexpr int NI = 4 / G;  // items per lane
   const unsigned i_raw = unsigned(p.first) + (blockIdx.x * BLOCK + threadIdx.x) / G;
   const int l = G == 1 ? 0 : int(threadIdx.x & (G - 1));
@@ -409,7 +437,6 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(const KConsts<float>* __restri
   if (G > 1 && i_raw >= end) return;
   const bool live = i_raw < end;
   const unsigned i = live ? i_raw : end - 1;
-  const KConsts<float>& k = *p.kc;
   const PhysConsts<float>& c = k.ph;
   const Tiles S(p);
   const uint32_t vo = env_off(i);
@@ -822,6 +849,18 @@ __global__ __launch_bounds__(BLOCK) void k_step_g(const KConsts<float>* __restri
   }
 }
 
+template <int KIND, bool CTBR, int G, bool SPEC>
+__global__ __launch_bounds__(BLOCK) void k_step_g(const KConsts<float>* __restrict__ kc, KParams p,
+                                                  const float4* __restrict__ act, QuadStepOut out) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
+  if constexpr (SPEC) {
+    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
+    step_g_body<KIND, CTBR, G>(K, p, act, out);
+  } else {
+    step_g_body<KIND, CTBR, G>(*kc, p, act, out);
+  }
+}
+
 template <int KIND, bool RELPOS>
 __global__ __launch_bounds__(BLOCK) void k_reset(KParams p, const uint8_t* __restrict__ mask,
                                                  float* __restrict__ obs_out) {
@@ -1118,6 +1157,7 @@ struct QuadHandle {
   uint32_t* stage = nullptr;  // [NFT][n] staging for host-side get/set_state, allocated on first use
   KConsts<float> kh;                 // host copy of the constant block
   KConsts<float>* kdev = nullptr;    // device copy the kernels read (scalar loads, K$-resident)
+  bool spec = false;                 // kh == a reference default block: k_step's SPEC form
 };
 
 namespace {
@@ -1150,70 +1190,7 @@ int quad_default_cfg(int32_t env_kind, int32_t wrapper, QuadCfg* c) {
   if (wrapper < QUAD_WRAP_NONE || wrapper > QUAD_WRAP_RELPOS) return fail(QUAD_EINVAL, "unknown wrapper");
   if (env_kind >= QUAD_ENV_BRAX_HOVER && wrapper != QUAD_WRAP_NONE)
     return fail(QUAD_EINVAL, "the brax env kinds take no wrapper");
-  std::memset(c, 0, sizeof *c);
-  c->env_kind = env_kind;
-  c->wrapper = wrapper;
-  c->auto_reset = 1;
-  const double pi = M_PI;
-  // HoverEnv._obs_bounds (hover_env.py:36-39) / _state_bounds (:54-57) share the angle/vel rows
-  const double ol[12] = {-4, -4, -2, -pi, -pi, -pi, -10, -10, -10, -6 * pi, -6 * pi, -6 * pi};
-  // _initial_state_bounds (hover_env.py:42-45; trajectory_follow_env.py:49-52)
-  const double il[12] = {-1.5, -1.5, 0.1, -0.3, -0.3, -0.3, -0.5, -0.5, -0.5, -0.5, -0.5, -0.5};
-  const double ih[12] = {1.5, 1.5, 1.5, 0.3, 0.3, 0.3, 0.5, 0.5, 0.5, 0.5, 0.5, 0.5};
-  for (int i = 0; i < 12; i++) {
-    c->obs_low[i] = float(ol[i]);
-    c->obs_high[i] = float(-ol[i]);
-    c->init_low[i] = float(il[i]);
-    c->init_high[i] = float(ih[i]);
-    c->term_low[i] = float(ol[i]);
-    c->term_high[i] = float(-ol[i]);
-  }
-  const double xy = env_kind == QUAD_ENV_TRAJ ? 3.0 : 2.0;  // traj :60-63, hover :54-57
-  c->term_low[0] = float(-xy); c->term_low[1] = float(-xy); c->term_low[2] = 0.f;
-  c->term_high[0] = float(xy); c->term_high[1] = float(xy); c->term_high[2] = float(xy);
-  c->max_episode_steps = env_kind == QUAD_ENV_TRAJ ? 2048 : 512;
-  c->nominal_voltage = env_kind == QUAD_ENV_TRAJ ? 16.8 : 8.4;
-  c->min_voltage = env_kind == QUAD_ENV_TRAJ ? 13.2 : 7.6;
-  const float tl[3] = {-1.5f, -1.5f, 0.3f}, th[3] = {1.5f, 1.5f, 1.8f};  // hover_env.py:48-51
-  for (int i = 0; i < 3; i++) { c->target_low[i] = tl[i]; c->target_high[i] = th[i]; }
-  c->max_motor_thrust = 13.0;  // drone_config.py:9-11,21
-  c->arm_length = 0.039799;
-  c->yaw_coeff = 0.0201;
-  c->max_torque = 0.5;
-  const float al[4] = {0.f, -0.5f, -0.5f, -0.5f}, ah[4] = {52.f, 0.5f, 0.5f, 0.5f};  // :60-65
-  for (int i = 0; i < 4; i++) { c->act_low[i] = al[i]; c->act_high[i] = ah[i]; }
-  c->vdrop_base = 0.01;
-  c->vdrop_load = 0.08;
-  c->rate_max_rad = 360.0 * (M_PI / 180.0);  // rate_wrapper.py:52, pid_gains.json:43-52
-  c->rate_kd[0] = 26; c->rate_kd[1] = 26; c->rate_kd[2] = 18;
-  c->rate_ki = 0.025;
-  c->rate_imax = 0.01;
-  c->inertia[0] = 4.16e-4; c->inertia[1] = 4.23e-4; c->inertia[2] = 5.37e-4;
-  c->timestep = 0.01;  // drone.xml:4
-  c->gravity[2] = -9.81;
-  c->density = 1.225;
-  c->viscosity = 1.8e-5;
-  {  // TrajectoryFollowEnv spline (trajectory_follow_env.py:25, :55-58, :199-203)
-    const float lo[3] = {-1.f, -1.f, 0.4f}, hi[3] = {1.f, 1.f, 1.4f}, amp[3] = {0.6f, 0.6f, 0.4f};
-    for (int i = 0; i < 3; i++) {
-      c->spline_center_low[i] = lo[i]; c->spline_center_high[i] = hi[i]; c->spline_amp[i] = amp[i];
-    }
-    c->spline_duration = 30.f;
-  }
-  if (env_kind >= QUAD_ENV_BRAX_HOVER) {  // train_brax_ppo.py
-    const bool traj = env_kind == QUAD_ENV_BRAX_TRAJ;
-    c->max_episode_steps = 500;                        // --episode-length (:436)
-    for (int i = 0; i < 3; i++) { c->target_low[i] = c->target_high[i] = i == 2 ? 1.f : 0.f; }  // (:55)
-    c->term_low[0] = c->term_low[1] = -3.f; c->term_high[0] = c->term_high[1] = 3.f;  // (:48-50)
-    c->term_low[2] = 0.02f; c->term_high[2] = 4.f;
-    c->reset_noise = 0.01f;                            // (:105-116, :271-272)
-    c->reward_pos_coef = traj ? 1.f : 2.f;             // (:146 / :338)
-    c->reward_action_coef = traj ? 0.001f : 0.f;       // (:339)
-    c->vel_limit = traj ? 20.f : 0.f;                  // (:190)
-    const float cen[3] = {0.f, 0.f, 1.f}, amp[3] = {0.5f, 0.5f, 0.2f}, fr[3] = {0.2f, 0.15f, 0.1f};
-    for (int i = 0; i < 3; i++) { c->traj_center[i] = cen[i]; c->traj_amp[i] = amp[i]; c->traj_freq[i] = fr[i]; }
-    c->traj_duration = 5.f;                            // --traj-duration-seconds (:444)
-  }
+  default_cfg_fill(env_kind, wrapper, c);
   return QUAD_OK;
 }
 
@@ -1246,6 +1223,8 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
     return fail(QUAD_EMODEL, why);
   }
   make_kconsts<float>(*cfg, h->pd, h->kh);
+  h->spec = is_default_block(h->kh, cfg->env_kind, cfg->wrapper == QUAD_WRAP_CTBR);
+  if (const char* v = std::getenv("QUADENV_SPEC")) h->spec = h->spec && std::atoi(v) != 0;
   h->device = device;
   h->n = n_envs;
   DeviceGuard g(device);
@@ -1289,6 +1268,8 @@ void quad_destroy(QuadHandle* h) {
 }
 
 int32_t quad_num_envs(const QuadHandle* h) { return h ? h->n : 0; }
+
+int32_t quad_kernel_form(const QuadHandle* h) { return h ? (h->lanes | (h->spec ? 16 : 0)) : -1; }
 
 int quad_seed(QuadHandle* h, uint64_t seed, void* stream) {
   if (!h) return fail(QUAD_EINVAL, "handle is NULL");
@@ -1357,28 +1338,33 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
       hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_TRAJ>), grid, blk, 0, s, h->kdev, kp, a, *out);
     else
       hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_HOVER>), grid, blk, 0, s, h->kdev, kp, a, *out);
-  } else if (G == 0) {  // legacy one-thread-per-env form with the LDS obs transpose (A/B reference)
+  } else if (G == 0) {  // one thread per env with the LDS obs transpose
     const dim3 grid(grid_of(count));
-    if (traj && ctbr)
-      hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, h->kdev, kp, a, *out);
-    else if (traj)
-      hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false>), grid, blk, 0, s, h->kdev, kp, a, *out);
-    else if (ctbr)
-      hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true>), grid, blk, 0, s, h->kdev, kp, a, *out);
-    else
-      hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false>), grid, blk, 0, s, h->kdev, kp, a, *out);
+#define QD_LAUNCH_K(SP)                                                                            \
+  if (traj && ctbr)                                                                             \
+    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);      \
+  else if (traj)                                                                                \
+    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);     \
+  else if (ctbr)                                                                                \
+    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);     \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);
+    if (h->spec) { QD_LAUNCH_K(true) } else { QD_LAUNCH_K(false) }
+#undef QD_LAUNCH_K
   } else {
     const dim3 grid(unsigned((int64_t(count) * G + BLOCK - 1) / BLOCK));
-#define QD_LAUNCH(GG)                                                                              \
+#define QD_LAUNCH(GG, SP)                                                                          \
   if (traj && ctbr)                                                                             \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, true, GG>), grid, blk, 0, s, h->kdev, kp, a, *out);   \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, true, GG, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);   \
   else if (traj)                                                                                \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, false, GG>), grid, blk, 0, s, h->kdev, kp, a, *out);  \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, false, GG, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);  \
   else if (ctbr)                                                                                \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, true, GG>), grid, blk, 0, s, h->kdev, kp, a, *out);  \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, true, GG, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);  \
   else                                                                                          \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG>), grid, blk, 0, s, h->kdev, kp, a, *out);
-    if (G == 1) { QD_LAUNCH(1) } else if (G == 2) { QD_LAUNCH(2) } else { QD_LAUNCH(4) }
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);
+    if (G == 1) {  // the batch-size default above 262,144 envs: SPEC form when the block is the default
+      if (h->spec) { QD_LAUNCH(1, true) } else { QD_LAUNCH(1, false) }
+    } else if (G == 2) { QD_LAUNCH(2, false) } else { QD_LAUNCH(4, false) }
 #undef QD_LAUNCH
   }
   HIP_TRY(hipGetLastError());
@@ -1402,7 +1388,7 @@ int quad_rollout(QuadHandle* h, const float* packed, const QuadRollout* r, void*
   RollArgs a{r->obs_copy, r->actions, r->log_prob, r->value, r->episode_starts, r->rewards, r->last_obs,
              r->last_start, r->ep_ret, r->ep_len, r->stats, uint32_t(r->rows), uint32_t(r->t0), r->steps,
              r->deterministic, r->seed, r->gamma};
-  HIP_TRY(launch_rollout(h->kdev, h->kp, h->cfg.env_kind, h->cfg.wrapper == QUAD_WRAP_CTBR, packed, a,
+  HIP_TRY(launch_rollout(h->kdev, h->kp, h->cfg.env_kind, h->cfg.wrapper == QUAD_WRAP_CTBR, h->spec, packed, a,
                          static_cast<hipStream_t>(stream)));
   return QUAD_OK;
 }
@@ -1448,14 +1434,17 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
   const dim3 grid(grid_of(h->n)), blk(BLOCK);
   float4* ao = reinterpret_cast<float4*>(actions_out);
   const bool traj = h->cfg.env_kind == QUAD_ENV_TRAJ, ctbr = h->cfg.wrapper == QUAD_WRAP_CTBR;
-  if (traj && ctbr)
-    hipLaunchKernelGGL((k_step_random<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-  else if (traj)
-    hipLaunchKernelGGL((k_step_random<QUAD_ENV_TRAJ, false>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-  else if (ctbr)
-    hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, true>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-  else
-    hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, false>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
+#define QD_LAUNCH_R(SP)                                                                                     \
+  if (traj && ctbr)                                                                                      \
+    hipLaunchKernelGGL((k_step_random<QUAD_ENV_TRAJ, true, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);   \
+  else if (traj)                                                                                         \
+    hipLaunchKernelGGL((k_step_random<QUAD_ENV_TRAJ, false, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
+  else if (ctbr)                                                                                         \
+    hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
+  else                                                                                                   \
+    hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
+  if (h->spec) { QD_LAUNCH_R(true) } else { QD_LAUNCH_R(false) }
+#undef QD_LAUNCH_R
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
 }

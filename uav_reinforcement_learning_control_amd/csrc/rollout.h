@@ -29,7 +29,7 @@ struct RollArgs {  // QuadRollout, flattened
 };
 
 // k_rollout<env_kind, ctbr> over all envs of kp (one 256-env block per CU-resident slot)
-hipError_t launch_rollout(const KConsts<float>* kc, const KParams& kp, int env_kind, bool ctbr,
+hipError_t launch_rollout(const KConsts<float>* kc, const KParams& kp, int env_kind, bool ctbr, bool spec,
                           const float* packed, const RollArgs& a, hipStream_t s);
 
 }  // namespace quadenv

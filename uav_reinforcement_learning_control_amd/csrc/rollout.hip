@@ -28,6 +28,7 @@
 
 #include "../../include/quadenv.h"
 #include "env_tiles.h"
+#include "kconsts_default.h"
 #include "policy_net.h"
 #include "quad_physics.h"
 #include "rollout.h"
@@ -106,10 +107,9 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, size_t row, 
 // l + 32 both carry env l & 31 (the same state, the same action, bit for bit), so the tile's X^T
 // fragment needs no exchange, and one wave's env step (VALU) can run under the other wave's MFMA.
 template <int KIND, bool CTBR, int NT>
-__global__ __launch_bounds__(512 / NT) void k_rollout(const KConsts<float>* __restrict__ kc, KParams p,
-                                                            const float* __restrict__ packed, RollArgs a) {
+__device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p, const float* __restrict__ packed,
+                                             RollArgs a) {
   constexpr int BLK = 512 / NT, WAVES = BLK / 64;
-  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
   extern __shared__ float lds[];
   __shared__ uint32_t renv[WAVES][64], rep[WAVES][64];
   const int w = threadIdx.x >> 6;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(512 / NT) void k_rollout(const KConsts<float>* __re
     for (int j = 0; j < 12; j++) r.obs[j] = fminf(fmaxf(ob[j] + 1e-3f * ac[j & 3], -1.f), 1.f);
     r.reward = ac[0]; r.term = false; r.trunc = false;
 #else
-    env_step<float, CTBR>(*p.kc, e, ac, r);
+    env_step<float, CTBR>(K, e, ac, r);
 #endif
     const bool done = r.term || r.trunc;
     // ---- TimeLimit bootstrap: r += gamma V(terminal_obs) (critic only if the wave holds one)
@@ -220,8 +220,8 @@ __global__ __launch_bounds__(512 / NT) void k_rollout(const KConsts<float>* __re
     reset_words_shfl<NT == 2 ? 63 : 31>(p, renv[w], rep[w], uint32_t(i), ep, owner && done, rs, u16);
     if (rs) {
       float init12[12], tgt[3], s12[12];
-      reset_affine_u(p.kc->init_lo, p.kc->init_span, p.kc->tgt_lo, p.kc->tgt_span, u16, init12, tgt);
-      env_reset_from<float, KIND>(*p.kc, e, init12, tgt, ob, s12);
+      reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
+      env_reset_from<float, KIND>(K, e, init12, tgt, ob, s12);
       ep += 1u;
     }
   }
@@ -251,7 +251,20 @@ __global__ __launch_bounds__(512 / NT) void k_rollout(const KConsts<float>* __re
   }
 }
 
-template <int KIND, bool CTBR, int NT>
+// SPEC: the handle's constant block is the reference default (kconsts_default.h): immediates
+template <int KIND, bool CTBR, int NT, bool SPEC>
+__global__ __launch_bounds__(512 / NT) void k_rollout(const KConsts<float>* __restrict__ kc, KParams p,
+                                                            const float* __restrict__ packed, RollArgs a) {
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
+  if constexpr (SPEC) {
+    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
+    rollout_body<KIND, CTBR, NT>(K, p, packed, a);
+  } else {
+    rollout_body<KIND, CTBR, NT>(*kc, p, packed, a);
+  }
+}
+
+template <int KIND, bool CTBR, int NT, bool SPEC>
 hipError_t launch(const KConsts<float>* kc, const KParams& kp, const float* packed, const RollArgs& a,
                   hipStream_t s) {
   static bool opted[64] = {};
@@ -259,34 +272,36 @@ hipError_t launch(const KConsts<float>* kc, const KParams& kp, const float* pack
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
   const int bytes = LDS_F * int(sizeof(float));
   if (!opted[dev]) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rollout<KIND, CTBR, NT>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_rollout<KIND, CTBR, NT, SPEC>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     if (e != hipSuccess) return e;
     opted[dev] = true;
   }
-  hipLaunchKernelGGL((k_rollout<KIND, CTBR, NT>), dim3((kp.n + RBLOCK - 1) / RBLOCK), dim3(512 / NT), bytes,
+  hipLaunchKernelGGL((k_rollout<KIND, CTBR, NT, SPEC>), dim3((kp.n + RBLOCK - 1) / RBLOCK), dim3(512 / NT), bytes,
                      s, kc, kp, packed, a);
   return hipGetLastError();
 }
 
 }  // namespace
 
-template <int NT>
+template <int NT, bool SPEC>
 hipError_t launch_nt(const KConsts<float>* kc, const KParams& kp, int env_kind, bool ctbr, const float* packed,
                      const RollArgs& a, hipStream_t s) {
   if (env_kind == QUAD_ENV_TRAJ)
-    return ctbr ? launch<QUAD_ENV_TRAJ, true, NT>(kc, kp, packed, a, s)
-                : launch<QUAD_ENV_TRAJ, false, NT>(kc, kp, packed, a, s);
-  return ctbr ? launch<QUAD_ENV_HOVER, true, NT>(kc, kp, packed, a, s)
-              : launch<QUAD_ENV_HOVER, false, NT>(kc, kp, packed, a, s);
+    return ctbr ? launch<QUAD_ENV_TRAJ, true, NT, SPEC>(kc, kp, packed, a, s)
+                : launch<QUAD_ENV_TRAJ, false, NT, SPEC>(kc, kp, packed, a, s);
+  return ctbr ? launch<QUAD_ENV_HOVER, true, NT, SPEC>(kc, kp, packed, a, s)
+              : launch<QUAD_ENV_HOVER, false, NT, SPEC>(kc, kp, packed, a, s);
 }
 
-hipError_t launch_rollout(const KConsts<float>* kc, const KParams& kp, int env_kind, bool ctbr,
+hipError_t launch_rollout(const KConsts<float>* kc, const KParams& kp, int env_kind, bool ctbr, bool spec,
                           const float* packed, const RollArgs& a, hipStream_t s) {
   const char* v = std::getenv("QUADENV_ROLLOUT_NT");  // A/B override: 1 or 2 tiles per wave
   const int nt = v && std::atoi(v) == 1 ? 1 : (v && std::atoi(v) == 2 ? 2 : ROLLOUT_NT_DEFAULT);
-  return nt == 1 ? launch_nt<1>(kc, kp, env_kind, ctbr, packed, a, s)
-                 : launch_nt<2>(kc, kp, env_kind, ctbr, packed, a, s);
+  if (nt == 1) return spec ? launch_nt<1, true>(kc, kp, env_kind, ctbr, packed, a, s)
+                           : launch_nt<1, false>(kc, kp, env_kind, ctbr, packed, a, s);
+  return spec ? launch_nt<2, true>(kc, kp, env_kind, ctbr, packed, a, s)
+              : launch_nt<2, false>(kc, kp, env_kind, ctbr, packed, a, s);
 }
 
 }  // namespace quadenv
