@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../../uav_reinforcement_learning_control_amd/csrc"
 make -s
 mkdir -p ../../tools/_build/obj
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on -fno-slp-vectorize"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on -fno-slp-vectorize -mllvm -amdgpu-kernarg-preload-count=16"
 O=../_lib/obj
 /opt/rocm/bin/hipcc $F -I$O -DQD_PROBE ${EXTRA:-} -c -o ../../tools/_build/obj/quadenv_probe.o quadenv.hip
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_build/probe.so \

@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/../../uav_reinforcement_learning_control_amd/csrc"
 make -s
 mkdir -p ../../tools/_build/obj
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on -fno-slp-vectorize"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on -fno-slp-vectorize -mllvm -amdgpu-kernarg-preload-count=16"
 O=../_lib/obj
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2

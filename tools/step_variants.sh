@@ -7,7 +7,7 @@ set -e
 cd "$(dirname "$0")/../uav_reinforcement_learning_control_amd/csrc"
 make -s
 mkdir -p ../../tools/_build/obj
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on -mllvm -amdgpu-kernarg-preload-count=16"
 O=../_lib/obj
 for v in PHYS2 NOPHYS NOOBS NORESET; do
   ( /opt/rocm/bin/hipcc $F -I$O -fno-slp-vectorize -DQD_ABL_$v -c -o ../../tools/_build/obj/quadenv_$v.o quadenv.hip &&

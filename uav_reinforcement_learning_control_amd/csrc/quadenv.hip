@@ -270,9 +270,15 @@ __device__ __forceinline__ void step_body(const KConsts<float>& K, KParams p, co
 // k_step: one env per thread. SPEC: the handle's constant block equals the reference default
 // (quad_create checks the bytes), so the constants are compiled in -- no scalar loads of the block
 // and no waits on them inside the step.
+// Kernel-argument preload (csrc/Makefile: -amdgpu-kernarg-preload-count=16): the leading scalar
+// arguments -- what the state loads need: tiles, their size, the env range, the actions -- arrive
+// in SGPRs at wave launch, so the loads are issued without first waiting on a scalar load of the
+// kernarg segment (the KParams / QuadStepOut aggregates behind them are not preloaded).
 template <int KIND, bool CTBR, bool SPEC>
-__global__ __launch_bounds__(BLOCK) void k_step(const KConsts<float>* __restrict__ kc, KParams p,
-                                                const float4* __restrict__ act, QuadStepOut out) {
+__global__ __launch_bounds__(BLOCK) void k_step(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
+                                                int32_t first, int32_t count, const KConsts<float>* __restrict__ kc,
+                                                KParams p, QuadStepOut out) {
+  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;
   p.kc = kc;  // noalias: constant-block loads stay scalar after the stores below (see KParams)
   __shared__ float4 lds[BLOCK * 3];
   __shared__ ResetLds rl;
@@ -850,8 +856,10 @@ __device__ __forceinline__ void step_g_body(const KConsts<float>& k, KParams p, 
 }
 
 template <int KIND, bool CTBR, int G, bool SPEC>
-__global__ __launch_bounds__(BLOCK) void k_step_g(const KConsts<float>* __restrict__ kc, KParams p,
-                                                  const float4* __restrict__ act, QuadStepOut out) {
+__global__ __launch_bounds__(BLOCK) void k_step_g(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
+                                                  int32_t first, int32_t count, const KConsts<float>* __restrict__ kc,
+                                                  KParams p, QuadStepOut out) {
+  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
   p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
   if constexpr (SPEC) {
     constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
@@ -1340,32 +1348,36 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
       hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_HOVER>), grid, blk, 0, s, h->kdev, kp, a, *out);
   } else if (G == 0) {  // one thread per env with the LDS obs transpose
     const dim3 grid(grid_of(count));
+#define QD_KARGS kp.tiles, a, kp.tile_bytes, kp.first, kp.count, h->kdev, kp, *out
 #define QD_LAUNCH_K(SP)                                                                            \
   if (traj && ctbr)                                                                             \
-    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);      \
+    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true, SP>), grid, blk, 0, s, QD_KARGS);      \
   else if (traj)                                                                                \
-    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);     \
+    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false, SP>), grid, blk, 0, s, QD_KARGS);     \
   else if (ctbr)                                                                                \
-    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);     \
+    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, QD_KARGS);     \
   else                                                                                          \
-    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);
+    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, QD_KARGS);
     if (h->spec) { QD_LAUNCH_K(true) } else { QD_LAUNCH_K(false) }
 #undef QD_LAUNCH_K
+#undef QD_KARGS
   } else {
     const dim3 grid(unsigned((int64_t(count) * G + BLOCK - 1) / BLOCK));
+#define QD_GARGS kp.tiles, a, kp.tile_bytes, kp.first, kp.count, h->kdev, kp, *out
 #define QD_LAUNCH(GG, SP)                                                                          \
   if (traj && ctbr)                                                                             \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, true, GG, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);   \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, true, GG, SP>), grid, blk, 0, s, QD_GARGS);   \
   else if (traj)                                                                                \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, false, GG, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);  \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, false, GG, SP>), grid, blk, 0, s, QD_GARGS);  \
   else if (ctbr)                                                                                \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, true, GG, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);  \
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, true, GG, SP>), grid, blk, 0, s, QD_GARGS);  \
   else                                                                                          \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG, SP>), grid, blk, 0, s, h->kdev, kp, a, *out);
+    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG, SP>), grid, blk, 0, s, QD_GARGS);
     if (G == 1) {  // the batch-size default above 262,144 envs: SPEC form when the block is the default
       if (h->spec) { QD_LAUNCH(1, true) } else { QD_LAUNCH(1, false) }
     } else if (G == 2) { QD_LAUNCH(2, false) } else { QD_LAUNCH(4, false) }
 #undef QD_LAUNCH
+#undef QD_GARGS
   }
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
