@@ -143,9 +143,10 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
                 int32_t n_envs, QuadHandle** out);
 void quad_destroy(QuadHandle* h);
 int32_t quad_num_envs(const QuadHandle* h);
-/* Diagnostics: the step-kernel form quad_create chose -- bits 0-3 lanes per env (0 = k_step, one
- * thread per env; 1/2/4 = k_step_g), bit 4 set when the handle's constant block is a reference
- * default and the kernels with compiled-in constants run (QUADENV_SPEC=0 turns that off). */
+/* Diagnostics: the step-kernel form quad_create chose -- bits 0-3 lanes per env (0 = one thread
+ * per env; 1/2/4 = k_step_g), bit 4 set when the handle's constant block is a reference default and
+ * the kernels with compiled-in constants run (QUADENV_SPEC=0 turns that off), bit 5 set when the
+ * one-thread form runs with helper waves drawing the resets (k_step_h; QUADENV_HELPER=0 turns it off). */
 int32_t quad_kernel_form(const QuadHandle* h);
 
 /* Re-key the reset RNG (HoverEnv.reset(seed=...), hover_env.py:210 -> gymnasium seeding) and

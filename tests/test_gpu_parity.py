@@ -101,11 +101,13 @@ def _pre12(st, i):
     return np.concatenate([st["qpos"][i][:3], np.zeros(3, np.float32), st["qvel"][i][:6]])
 
 
-@pytest.fixture(params=["1", "2", "4", "0"])
+@pytest.fixture(params=["1", "2", "4", "0", "0n"])
 def kernel_variant(request, monkeypatch):
-    """Every step kernel form must be exact: k_step_g with 1 (default), 2 or 4 lanes per env,
-    and the legacy one-thread-per-env k_step with an LDS obs transpose (QUADENV_LANES=0)."""
-    monkeypatch.setenv("QUADENV_LANES", request.param)
+    """Every step kernel form must be exact: k_step_g with 1, 2 or 4 lanes per env, and the
+    one-thread-per-env form (QUADENV_LANES=0) with helper waves drawing the resets (k_step_h, the
+    default below 262,144 envs) and without them ("0n": k_step)."""
+    monkeypatch.setenv("QUADENV_LANES", request.param[0])
+    monkeypatch.setenv("QUADENV_HELPER", "0" if request.param.endswith("n") else "1")
     return request.param
 
 
@@ -119,17 +121,17 @@ def spec_mode(request, monkeypatch):
 
 def test_kernel_form_selection(spec_mode):
     from uav_reinforcement_learning_control_amd import _native as N
-    for n, lanes in ((4096, 0), (65536, 0), (300000, 1)):
+    for n, form in ((4096, 32), (65536, 32), (300000, 1)):  # 32: helper waves (k_step_h)
         e = _env(n)
-        assert N.lib().quad_kernel_form(e._h) == lanes | (16 if spec_mode == "1" else 0), n
+        assert N.lib().quad_kernel_form(e._h) == form | (16 if spec_mode == "1" else 0), n
         e.close()
     for kw in (dict(max_episode_steps=100), dict(cfg_overrides=dict(density=1.0))):
         e = _env(1024, **kw)  # not the reference default: generic kernels
-        assert N.lib().quad_kernel_form(e._h) == 0
+        assert N.lib().quad_kernel_form(e._h) == 32
         e.close()
     for env_name, wrapper in (("hover", "RateControlWrapper"), ("trajectory", None), ("trajectory", "RateControlWrapper")):
         e = _env(1024, env_name, wrapper)
-        assert N.lib().quad_kernel_form(e._h) == (16 if spec_mode == "1" else 0), (env_name, wrapper)
+        assert N.lib().quad_kernel_form(e._h) == 32 | (16 if spec_mode == "1" else 0), (env_name, wrapper)
         e.close()
 
 

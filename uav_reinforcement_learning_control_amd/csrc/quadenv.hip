@@ -235,7 +235,12 @@ __device__ __forceinline__ void step_body(const KConsts<float>& K, KParams p, co
     rs_probe = rs;
 #endif
     float u16[16];
+#if defined(QD_ABL_NODRAW)  // cost ablation (tools only): the reset without its Philox draw / LDS hand-off
+#pragma unroll
+    for (int j = 0; j < 16; j++) u16[j] = 0.5f;
+#else
     reset_words_wave(p, rl, uint32_t(i), ep, rs, u16);
+#endif
     if (stamps && rs) QD_PIN_N(u16, 16);
     QD_STAMP(stamps, 8);
     if (rs) {
@@ -265,6 +270,125 @@ __device__ __forceinline__ void step_body(const KConsts<float>& K, KParams p, co
     dst[15] = __popcll(__ballot(rs_probe));
   }
 #endif
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_step_h<KIND, CTBR, SPEC>: the step with HELPER waves. A 512-thread block owns 256 envs: waves
+// 0-3 step one env per lane exactly as k_step; waves 4-7 -- one beside each step wave on its SIMD --
+// meanwhile draw every env's NEXT reset (the Philox words of its episode counter, the affine map,
+// the quaternion, the reset observation: reset_block / reset_affine_u / env_reset_from, the same
+// functions, so the same bits) into an LDS image, and after the block barrier a resetting step lane
+// only copies its row. The draw had been on the lone step wave's path (0.72 us of a 6.5 us step at
+// 65,536 envs, ablation build); the helpers run it in the issue slots the stalled step wave leaves.
+constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
+template <int KIND, bool CTBR>
+__device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, const float4* __restrict__ act,
+                                            QuadStepOut out, float4* lds, float* H) {
+  const int tid = threadIdx.x;
+  const int block_first = p.first + blockIdx.x * BLOCK;
+  const int end = p.first + p.count;
+  const int l = tid & (BLOCK - 1);
+  const bool live = block_first + l < end;
+  const int i = live ? block_first + l : end - 1;
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
+  if (tid >= BLOCK) {  // ---- helper: env i's next reset, into H[f][l]
+    const uint32_t ep = S.ldu(F_EP, vo);
+    float u16[16];
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      uint32_t c[4];
+      reset_block(p.seed, p.gid_base + uint64_t(i), ep, b, c);
+#pragma unroll
+      for (int j = 0; j < 4; j++) u16[4 * b + j] = u01(c[j]);
+    }
+    float init12[12], tgt[3], obs[12], s12[12];
+    reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
+    EnvRegs<float> e;
+    env_reset_from<float, KIND>(K, e, init12, tgt, obs, s12);
+    const float row[HROW] = {e.pos[0], e.pos[1], e.pos[2], e.q[0], e.q[1], e.q[2], e.q[3],
+                             e.v[0], e.v[1], e.v[2], e.w[0], e.w[1], e.w[2],
+                             e.target[0], e.target[1], e.target[2],
+                             obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9],
+                             obs[10], obs[11]};
+#pragma unroll
+    for (int f = 0; f < HROW; f++) H[f * BLOCK + l] = row[f];
+    __syncthreads();  // (1) the image is complete
+    __syncthreads();  // (2) the obs rows are staged
+  } else {  // ---- step
+    float obs[12];
+    EnvRegs<float> e;
+    load_env(p, i, e, CTBR);
+    const uint32_t ep = S.ldu(F_EP, vo);
+    const float4 a4 = act[i];
+    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+    StepRes r;
+    env_step<float, CTBR>(K, e, a, r);
+    settle(ep);
+    const uint32_t o = uint32_t(i) * 4u;
+    if (live) {
+      sto(out.reward, o, r.reward);
+      sto(out.terminated, uint32_t(i), uint8_t(r.term));
+      sto(out.truncated, uint32_t(i), uint8_t(r.trunc));
+      if (out.motor_commands)
+        sto(reinterpret_cast<float4*>(out.motor_commands), 4u * o,
+            make_float4(r.motor[0], r.motor[1], r.motor[2], r.motor[3]));
+      if (out.voltage_scale) sto(out.voltage_scale, o, r.vscale);
+      if (out.state12) store_row12(out.state12, uint32_t(i), r.state12);
+      if (out.target_info) {
+        float info[9];
+        target_info_of<KIND>(K, p, i, e, ep, info);
+        store_target_info(out.target_info, i, info);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
+    const bool rs = live && (r.term || r.trunc) && p.auto_reset;
+    __syncthreads();  // (1)
+    if (rs) {
+      if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
+      float row[HROW];
+#pragma unroll
+      for (int f = 0; f < HROW; f++) row[f] = H[f * BLOCK + l];
+#pragma unroll
+      for (int j = 0; j < 3; j++) {
+        e.pos[j] = row[j]; e.v[j] = row[7 + j]; e.w[j] = row[10 + j]; e.target[j] = row[13 + j];
+        e.rint[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++) { e.q[j] = row[3 + j]; e.th[j] = 0.f; e.s[j] = 0.f; }
+#pragma unroll
+      for (int j = 0; j < 12; j++) obs[j] = row[16 + j];
+      e.volt = float(K.vnom);
+      e.step = 0;
+      S.stu(F_EP, vo, ep + 1u);
+    }
+    if (live) store_env(p, i, e, CTBR);
+    lds[3 * l + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
+    lds[3 * l + 1] = make_float4(obs[4], obs[5], obs[6], obs[7]);
+    lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
+    __syncthreads();  // (2)
+  }
+  // the block's [256,12] obs rows as contiguous float4 stores, shared by all 512 threads
+  const int nf4 = min(BLOCK, end - block_first) * 3;
+  float4* dst = reinterpret_cast<float4*>(out.obs + size_t(block_first) * 12);
+  for (int idx = tid; idx < nf4; idx += 2 * BLOCK) dst[idx] = lds[idx];
+}
+
+template <int KIND, bool CTBR, bool SPEC>
+__global__ __launch_bounds__(2 * BLOCK) void k_step_h(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
+                                                      int32_t first, int32_t count,
+                                                      const KConsts<float>* __restrict__ kc, KParams p, QuadStepOut out) {
+  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
+  p.kc = kc;
+  __shared__ float4 lds[BLOCK * 3];
+  __shared__ float H[HROW * BLOCK];
+  if constexpr (SPEC) {
+    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
+    step_h_body<KIND, CTBR>(K, p, act, out, lds, H);
+  } else {
+    step_h_body<KIND, CTBR>(*kc, p, act, out, lds, H);
+  }
 }
 
 // k_step: one env per thread. SPEC: the handle's constant block equals the reference default
@@ -1166,6 +1290,7 @@ struct QuadHandle {
   KConsts<float> kh;                 // host copy of the constant block
   KConsts<float>* kdev = nullptr;    // device copy the kernels read (scalar loads, K$-resident)
   bool spec = false;                 // kh == a reference default block: k_step's SPEC form
+  bool helper = true;                // one-thread form: k_step_h (helper waves draw the resets)
 };
 
 namespace {
@@ -1233,6 +1358,9 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   make_kconsts<float>(*cfg, h->pd, h->kh);
   h->spec = is_default_block(h->kh, cfg->env_kind, cfg->wrapper == QUAD_WRAP_CTBR);
   if (const char* v = std::getenv("QUADENV_SPEC")) h->spec = h->spec && std::atoi(v) != 0;
+  // measured: helper waves 6.54 -> 5.87 us at 65,536 envs, 5.74 -> 4.24 at 4,096;
+  // QUADENV_HELPER=0 keeps the plain k_step (A/B and tests)
+  if (const char* v = std::getenv("QUADENV_HELPER")) h->helper = std::atoi(v) != 0;
   h->device = device;
   h->n = n_envs;
   DeviceGuard g(device);
@@ -1277,7 +1405,9 @@ void quad_destroy(QuadHandle* h) {
 
 int32_t quad_num_envs(const QuadHandle* h) { return h ? h->n : 0; }
 
-int32_t quad_kernel_form(const QuadHandle* h) { return h ? (h->lanes | (h->spec ? 16 : 0)) : -1; }
+int32_t quad_kernel_form(const QuadHandle* h) {
+  return h ? (h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0)) : -1;
+}
 
 int quad_seed(QuadHandle* h, uint64_t seed, void* stream) {
   if (!h) return fail(QUAD_EINVAL, "handle is NULL");
@@ -1358,8 +1488,21 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, QD_KARGS);     \
   else                                                                                          \
     hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, QD_KARGS);
-    if (h->spec) { QD_LAUNCH_K(true) } else { QD_LAUNCH_K(false) }
+#define QD_LAUNCH_H(SP)                                                                            \
+  if (traj && ctbr)                                                                             \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, true, SP>), grid, blk2, 0, s, QD_KARGS);      \
+  else if (traj)                                                                                \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, false, SP>), grid, blk2, 0, s, QD_KARGS);     \
+  else if (ctbr)                                                                                \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, true, SP>), grid, blk2, 0, s, QD_KARGS);     \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, false, SP>), grid, blk2, 0, s, QD_KARGS);
+    const dim3 blk2(2 * BLOCK);
+    if (h->helper) {
+      if (h->spec) { QD_LAUNCH_H(true) } else { QD_LAUNCH_H(false) }
+    } else if (h->spec) { QD_LAUNCH_K(true) } else { QD_LAUNCH_K(false) }
 #undef QD_LAUNCH_K
+#undef QD_LAUNCH_H
 #undef QD_KARGS
   } else {
     const dim3 grid(unsigned((int64_t(count) * G + BLOCK - 1) / BLOCK));
