@@ -201,7 +201,9 @@ def _kstep_rate(n, steps, dev, seed) -> dict:
     resets = float((r["terminated"] | r["truncated"]).float().mean())
     del r
     e.close()
-    return {"envs": n, "steps_per_launch": steps, "kernel": "k_step_random<HOVER,noCTBR>",
+    return {"envs": n, "steps_per_launch": steps,
+            "kernel": "k_step_random_h<HOVER,noCTBR> (helper waves draw actions and resets)"
+            if os.environ.get("QUADENV_HELPER", "1") != "0" else "k_step_random<HOVER,noCTBR>",
             "us_per_step": us, "env_steps_per_s": n / (us * 1e-6), "reset_fraction_per_step": resets,
             "bytes_per_env_step_out": 70, "note": "state read/written once per launch; actions drawn in-kernel"}
 
@@ -614,7 +616,8 @@ def main():
         "device_us_per_step": res["region_us"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_step<HOVER,noCTBR>", "kernel_us": kus,
+                     "kernel": "k_step_h<HOVER,noCTBR> (helper waves draw the resets)"
+                     if os.environ.get("QUADENV_HELPER", "1") != "0" else "k_step<HOVER,noCTBR>", "kernel_us": kus,
                      "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs,
                      "issue": _pmc_issue(args.envs)},
     }

@@ -598,7 +598,9 @@ def test_invalid_arguments_fail_cleanly():
 
 
 @pytest.mark.parametrize("env_name,wrapper", [("hover", None), ("trajectory", "RateControlWrapper")])
-def test_step_random_is_the_step_by_step_rollout(env_name, wrapper, spec_mode):
+@pytest.mark.parametrize("helper", ["1", "0"])
+def test_step_random_is_the_step_by_step_rollout(env_name, wrapper, spec_mode, helper, monkeypatch):
+    monkeypatch.setenv("QUADENV_HELPER", helper)  # k_step_random_h (default) / k_step_random
     """quad_step_random (config 2 in one launch, state on chip) == random_actions + quad_step
     step by step, bit for bit: every step's obs, reward, flags, terminal obs, the actions, and the
     final state (incl. episode counters after the auto-resets it crossed)."""

@@ -471,6 +471,151 @@ __device__ __forceinline__ void step_random_body(const KConsts<float>& K, KParam
   }
 }
 
+// The same with helper waves (see k_step_h): a 512-thread block owns 256 envs; waves 0-3 step them,
+// waves 4-7 draw -- two steps ahead -- each env's actions (quad_random_actions' Philox map) into a
+// double-buffered LDS slot, and keep each env's next-reset row (k_step_h's image) current: after
+// every step they read which envs reset, advance those episode counters and redraw their rows.
+// Per step: barrier A (flags known; the image is current) -> resets copied, obs rows staged ->
+// barrier B -> obs rows stored by all 512 threads, helpers redraw. Same bits as k_step_random.
+template <int KIND, bool CTBR>
+__device__ __forceinline__ void helper_reset_row(const KConsts<float>& K, const KParams& p, int i, uint32_t ep,
+                                                 float* H, int l) {
+  float u16[16];
+#pragma unroll
+  for (uint32_t b = 0; b < 4; b++) {
+    uint32_t c[4];
+    reset_block(p.seed, p.gid_base + uint64_t(i), ep, b, c);
+#pragma unroll
+    for (int j = 0; j < 4; j++) u16[4 * b + j] = u01(c[j]);
+  }
+  float init12[12], tgt[3], obs[12], s12[12];
+  reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
+  EnvRegs<float> e;
+  env_reset_from<float, KIND>(K, e, init12, tgt, obs, s12);
+  const float row[HROW] = {e.pos[0], e.pos[1], e.pos[2], e.q[0], e.q[1], e.q[2], e.q[3],
+                           e.v[0], e.v[1], e.v[2], e.w[0], e.w[1], e.w[2],
+                           e.target[0], e.target[1], e.target[2],
+                           obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9],
+                           obs[10], obs[11]};
+#pragma unroll
+  for (int f = 0; f < HROW; f++) H[f * BLOCK + l] = row[f];
+}
+
+// a resetting step lane takes its row of the helper image (k_step_h, k_step_random_h)
+template <int KIND>
+__device__ __forceinline__ void take_reset_row(const KConsts<float>& K, const float* H, int l, EnvRegs<float>& e,
+                                               float obs[12]) {
+  float row[HROW];
+#pragma unroll
+  for (int f = 0; f < HROW; f++) row[f] = H[f * BLOCK + l];
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    e.pos[j] = row[j]; e.v[j] = row[7 + j]; e.w[j] = row[10 + j]; e.target[j] = row[13 + j];
+    e.rint[j] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) { e.q[j] = row[3 + j]; e.th[j] = 0.f; e.s[j] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < 12; j++) obs[j] = row[16 + j];
+  e.volt = float(K.vnom);
+  e.step = 0;
+}
+
+__device__ __forceinline__ float4 random_action4(uint64_t seed, uint64_t gid, uint32_t step) {
+  uint32_t c[4] = {uint32_t(gid), uint32_t(gid >> 32), step, 0x100u};
+  philox4x32_10(c, uint32_t(seed), uint32_t(seed >> 32));
+  return make_float4(float(c[0] >> 8) * 0x1p-23f - 1.0f, float(c[1] >> 8) * 0x1p-23f - 1.0f,
+                     float(c[2] >> 8) * 0x1p-23f - 1.0f, float(c[3] >> 8) * 0x1p-23f - 1.0f);
+}
+
+template <int KIND, bool CTBR>
+__device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KParams p, QuadStepOut out,
+                                                   float4* __restrict__ act_out, uint32_t step0, int32_t steps,
+                                                   float4* lds, float* H, float4* A, uint32_t* R) {
+  const int tid = threadIdx.x;
+  const int block_first = blockIdx.x * BLOCK;
+  const int n = p.n;
+  const int l = tid & (BLOCK - 1);
+  const bool live = block_first + l < n;
+  const int i = live ? block_first + l : n - 1;
+  const Tiles S(p);
+  const uint32_t vo = env_off(uint32_t(i));
+  const uint64_t gid = p.gid_base + uint64_t(i);
+  const bool helper = tid >= BLOCK;
+  const int nf4 = min(BLOCK, n - block_first) * 3;
+  EnvRegs<float> e;
+  uint32_t ep = 0;
+  if (helper) {
+    ep = S.ldu(F_EP, vo);
+    A[l] = random_action4(p.seed, gid, step0);
+    if (steps > 1) A[BLOCK + l] = random_action4(p.seed, gid, step0 + 1u);
+    helper_reset_row<KIND, CTBR>(K, p, i, ep, H, l);
+  } else {
+    load_env(p, i, e, CTBR);
+  }
+  __syncthreads();
+  for (int t = 0; t < steps; t++) {
+    const uint32_t row = uint32_t(t) * uint32_t(n) + uint32_t(i);  // time-major row (< 2^32: checked)
+    if (!helper) {
+      const float4 a4 = A[(t & 1) * BLOCK + l];
+      const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+      StepRes r;
+      env_step<float, CTBR>(K, e, a, r);
+      if (live) {
+        sto(out.reward, 4u * row, r.reward);
+        sto(out.terminated, row, uint8_t(r.term));
+        sto(out.truncated, row, uint8_t(r.trunc));
+      }
+      float obs[12];
+#pragma unroll
+      for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
+      const bool rs = live && (r.term || r.trunc) && p.auto_reset;
+      __syncthreads();  // (A) the image holds every env's next reset
+      if (rs) {
+        if (out.terminal_obs) store_row12(out.terminal_obs, row, r.obs);
+        take_reset_row<KIND>(K, H, l, e, obs);
+      }
+      R[l] = rs ? 1u : 0u;
+      lds[3 * l + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
+      lds[3 * l + 1] = make_float4(obs[4], obs[5], obs[6], obs[7]);
+      lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
+      __syncthreads();  // (B) obs rows and reset flags staged
+    } else {
+      if (act_out && live) sto(act_out, 16u * row, A[(t & 1) * BLOCK + l]);
+      __syncthreads();  // (A)
+      __syncthreads();  // (B)
+      if (R[l]) {  // this env reset at step t: its next episode's row
+        ep += 1u;
+        helper_reset_row<KIND, CTBR>(K, p, i, ep, H, l);
+      }
+      if (t + 2 < steps) A[(t & 1) * BLOCK + l] = random_action4(p.seed, gid, step0 + uint32_t(t + 2));
+    }
+    float4* dst = reinterpret_cast<float4*>(out.obs + (size_t(t) * size_t(n) + size_t(block_first)) * 12);
+    for (int idx = tid; idx < nf4; idx += 2 * BLOCK) dst[idx] = lds[idx];
+  }
+  if (live) {
+    if (helper) S.stu(F_EP, vo, ep);
+    else store_env(p, i, e, CTBR);
+  }
+}
+
+template <int KIND, bool CTBR, bool SPEC>
+__global__ __launch_bounds__(2 * BLOCK) void k_step_random_h(const KConsts<float>* __restrict__ kc, KParams p,
+                                                             QuadStepOut out, float4* __restrict__ act_out,
+                                                             uint32_t step0, int32_t steps) {
+  p.kc = kc;
+  __shared__ float4 lds[BLOCK * 3];
+  __shared__ float H[HROW * BLOCK];
+  __shared__ float4 A[2 * BLOCK];
+  __shared__ uint32_t R[BLOCK];
+  if constexpr (SPEC) {
+    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
+    step_random_h_body<KIND, CTBR>(K, p, out, act_out, step0, steps, lds, H, A, R);
+  } else {
+    step_random_h_body<KIND, CTBR>(*kc, p, out, act_out, step0, steps, lds, H, A, R);
+  }
+}
+
 template <int KIND, bool CTBR, bool SPEC>
 __global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __restrict__ kc, KParams p,
                                                        QuadStepOut out, float4* __restrict__ act_out,
@@ -1598,8 +1743,21 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
     hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
   else                                                                                                   \
     hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-  if (h->spec) { QD_LAUNCH_R(true) } else { QD_LAUNCH_R(false) }
+#define QD_LAUNCH_RH(SP)                                                                                     \
+  if (traj && ctbr)                                                                                      \
+    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_TRAJ, true, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);   \
+  else if (traj)                                                                                         \
+    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_TRAJ, false, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
+  else if (ctbr)                                                                                         \
+    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, true, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
+  else                                                                                                   \
+    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, false, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
+  const dim3 blk2(2 * BLOCK);
+  if (h->helper) {
+    if (h->spec) { QD_LAUNCH_RH(true) } else { QD_LAUNCH_RH(false) }
+  } else if (h->spec) { QD_LAUNCH_R(true) } else { QD_LAUNCH_R(false) }
 #undef QD_LAUNCH_R
+#undef QD_LAUNCH_RH
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
 }
