@@ -95,6 +95,14 @@ def _bucket_bound(params, flat: torch.Tensor) -> bool:
     return True
 
 
+def _rccl_has_avg() -> bool:
+    """ncclAvg exists from NCCL 2.10 (RCCL follows the NCCL API versions)."""
+    try:
+        return tuple(torch.cuda.nccl.version()[:2]) >= (2, 10)
+    except Exception:
+        return False
+
+
 def allreduce_mean_(params, flat: torch.Tensor, world: int) -> None:
     """Average the gradients of `params` over ranks with ONE all_reduce of a flat fp32 bucket.
     With the .grad tensors bound to the bucket (bind_grad_bucket) the collective runs in place;
@@ -106,7 +114,7 @@ def allreduce_mean_(params, flat: torch.Tensor, world: int) -> None:
             k = p.numel()
             flat[off:off + k].copy_(p.grad.reshape(-1))
             off += k
-    if dist.get_backend() == "nccl":
+    if dist.get_backend() == "nccl" and _rccl_has_avg():
         dist.all_reduce(flat, op=dist.ReduceOp.AVG)   # RCCL: the mean in the collective itself
     else:
         dist.all_reduce(flat, op=dist.ReduceOp.SUM)   # gloo has no AVG
