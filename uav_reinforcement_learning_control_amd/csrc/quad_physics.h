@@ -395,6 +395,10 @@ QD_HD void forward_acc(const PhysConsts<T>& c, const T qn[4], const T th[4], con
   // (written as explicit fma chains: -ffp-contract=on fuses only within one expression, and the
   // cross products, frame rotations and accumulations below are ~1/3 of the physics)
   T Qs[4];
+#if defined(QD_ABL_NOPROPS)  // cost ablation (tools only): no prop drag terms
+  Qs[0] = Qs[1] = Qs[2] = Qs[3] = T(0);
+  if (false)
+#endif
 #pragma unroll
   for (int p = 0; p < 4; p++) {
     T sn, cs;
