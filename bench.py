@@ -93,6 +93,16 @@ def _gated_kernel_us(step, actions, n_launch: int = 200) -> float:
     return e0.elapsed_time(e1) * 1e3 / (max(1, n_launch // chunk) * chunk)
 
 
+def _kernel_name(env) -> str:
+    """The step kernel form the handle actually launches (quad_kernel_form: lanes | 16 SPEC | 32 helper)."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    form = int(N.lib().quad_kernel_form(env._h))
+    lanes = form & 15
+    name = (f"k_step_g<{lanes}>" if lanes else ("k_step_h" if form & 32 else "k_step")) + "<HOVER,noCTBR>"
+    tags = (["SPEC constants"] if form & 16 else []) + (["helper waves draw the resets"] if form & 32 else [])
+    return name + (f" ({', '.join(tags)})" if tags else "")
+
+
 def _run_rank(args, rank, world, local_rank):
     from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
 
@@ -138,7 +148,8 @@ def _run_rank(args, rank, world, local_rank):
 
     # per-launch kernel time (roofline) on the same kernel, stream and data
     res = dict(elapsed=elapsed, region_us=region_us,
-               kernel_us=_gated_kernel_us(step, actions, args.kernel_launches))
+               kernel_us=_gated_kernel_us(step, actions, args.kernel_launches),
+               kernel=_kernel_name(env))
     if args.rollout_steps > 0:
         res["rollout"] = _rollout_phase(env, args)
     if args.e2e_iters > 0:
@@ -616,8 +627,7 @@ def main():
         "device_us_per_step": res["region_us"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_step_h<HOVER,noCTBR> (helper waves draw the resets)"
-                     if os.environ.get("QUADENV_HELPER", "1") != "0" else "k_step<HOVER,noCTBR>", "kernel_us": kus,
+                     "kernel": res["kernel"], "kernel_us": kus,
                      "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs,
                      "issue": _pmc_issue(args.envs)},
     }

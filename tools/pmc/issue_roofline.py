@@ -3,9 +3,10 @@
 profiles/pmc_issue.json (bench.py reads the latter into roofline.issue).
 
 Per step-kernel dispatch (median over dispatches 20..end, past the post-reset transient):
-  instructions per wave by class (SQ_INSTS_*), i.e. per 64 env-steps (one env per lane);
-  the lone-wave issue floor: a wave issues at most one vector instruction per 4 cycles
-  (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so one wave per SIMD needs
+  instructions per 64 env-steps by class (SQ_INSTS_* / (envs / 64)): one step wave of 64 envs,
+  plus -- in the helper-wave forms (k_step_h) -- the helper wave that shares its SIMD;
+  the per-SIMD issue floor: a SIMD issues at most one wave64 vector instruction per 4 cycles
+  (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so the SIMD that holds those waves needs
   >= 4 * (VALU + VMEM + LDS) cycles + SALU/SMEM/branch slots;
   wave cycles and their split (SQ_WAVE_CYCLES = WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY,
   quad-cycles), VALU-active share, and the effective clock GRBM_GUI_ACTIVE / 8 / kernel time."""
@@ -55,21 +56,22 @@ def main(root="gpurun_out/issue", rnd="r02"):
         key = max(d, key=lambda k: len(d[k]))
         c = {k: statistics.median(v[20:] or v) for k, v in d[key].items()}
         waves = c.get("SQ_WAVES", 0) or 1
-        per_wave = {k[len("SQ_INSTS_"):].lower(): c[k] / waves for k in c if k.startswith("SQ_INSTS_")}
+        units = n / 64  # SIMD slots: one step wave (+ its helper wave) per 64 envs
+        per_wave = {k[len("SQ_INSTS_"):].lower(): c[k] / units for k in c if k.startswith("SQ_INSTS_")}
         vec = per_wave.get("valu", 0) + per_wave.get("vmem_rd", 0) + per_wave.get("vmem_wr", 0) + per_wave.get("lds", 0)
         sca = per_wave.get("salu", 0) + per_wave.get("smem", 0) + per_wave.get("branch", 0)
         us = traces.get(n)
-        r = {"kernel": key[0], "grid": key[1], "envs": n, "waves": waves,
-             "instructions_per_wave": per_wave, "vector_instructions_per_wave": vec,
-             "scalar_instructions_per_wave": sca, "kernel_us_rocprof_trace": us}
+        r = {"kernel": key[0], "grid": key[1], "envs": n, "waves": waves, "waves_per_64_envs": waves / units,
+             "instructions_per_64_env_steps": per_wave, "vector_instructions_per_64_env_steps": vec,
+             "scalar_instructions_per_64_env_steps": sca, "kernel_us_rocprof_trace": us}
         if "SQ_WAVE_CYCLES" in c:
-            wc = c["SQ_WAVE_CYCLES"] * 4 / waves  # quad-cycles -> cycles, per wave
+            wc = c["SQ_WAVE_CYCLES"] * 4 / waves  # quad-cycles -> cycles, mean wave lifetime
             r["wave_cycles"] = wc
             for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU",
                       "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_MISC"):
                 if k in c:
                     r[k.lower() + "_share"] = c[k] * 4 / waves / wc
-            # lone-wave issue floor vs the measured wave lifetime (same counters, same dispatches)
+            # per-SIMD issue floor vs the measured wave lifetime (same counters, same dispatches)
             r["issue_floor_cycles"] = 4 * vec + sca
             r["frac_issue_floor"] = r["issue_floor_cycles"] / wc
         if us and "GRBM_GUI_ACTIVE" in c:
