@@ -14,6 +14,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 from collections import defaultdict
@@ -26,7 +27,8 @@ def load(root):
         rows.sort(key=lambda r: int(r.get("Dispatch_Id", r.get("Correlation_Id", 0)) or 0))
         for r in rows:
             grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
-            d[(r["Kernel_Name"].split("(")[0], grid)][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            m = re.search(r"k_\w+<[^>]*>", r["Kernel_Name"])
+            d[(m.group(0) if m else r["Kernel_Name"], grid)][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return d
 
 
@@ -75,7 +77,11 @@ def main(root="gpurun_out/issue", rnd="r02"):
             r["issue_floor_cycles"] = 4 * vec + sca
             r["frac_issue_floor"] = r["issue_floor_cycles"] / wc
         if us and "GRBM_GUI_ACTIVE" in c:
-            r["effective_clock_GHz"] = c["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3)
+            # GRBM_GUI_ACTIVE per XCD over the traced kernel time; above the 2.4 GHz peak clock it
+            # holds profiler serialization around a short dispatch and is not a clock
+            clk = c["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3)
+            if clk <= 2.5:
+                r["effective_clock_GHz"] = clk
         res[str(n)] = r
     for d in (os.path.join("profiles", rnd), "profiles"):
         os.makedirs(d, exist_ok=True)
