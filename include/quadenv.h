@@ -399,6 +399,10 @@ int quad_clip_adam(const QuadAdam* a, void* workspace, int64_t workspace_bytes, 
 
 /* Device workspace (bytes) quad_ppo_grad needs for a minibatch of `batch` rows. */
 int64_t quad_ppo_workspace_bytes(int32_t batch);
+/* Which kernel quad_ppo_grad launches: 1 = k_ppo_grad_x3 (bf16 MFMA on three-piece splits of every
+ * f32 operand, f32-level error; the default), 0 = k_ppo_grad (f32-input MFMA; environment
+ * QUADENV_LEARNER=f32, read on every call). Both meet the same accuracy bar. */
+int quad_ppo_grad_form(void);
 int quad_ppo_grad(const QuadPolicyParams* params, const QuadPPOBatch* b, const QuadPolicyGrads* grads,
                   void* workspace, int64_t workspace_bytes, void* stream);
 

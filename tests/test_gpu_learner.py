@@ -8,7 +8,12 @@ err_torch32 is the error of torch's own fp32 autograd on the same inputs (a stro
 over 262,144 rows has max|g| far below the sum of |terms|, so torch's error sets the scale there).
 Ratios are placed at least 1e-3 away from the clip bounds so that no implementation's rounding can
 flip a clipping decision; the exact in-range tie of min(A r, A clip(r)) follows torch (half the
-gradient to each side). Loss statistics to 1e-4 relative.
+gradient to each side). Likewise the minibatch rows are drawn from those whose float64 hidden
+pre-activations (both nets, both layers) are all at least 1e-5 away from zero: a ReLU decision on a
+pre-activation within f32 rounding of zero flips between any two f32 implementations (torch fp32
+included: measured 1e-4..2e-2 relative gradient differences on unfiltered 65,536 / 262,144-row
+minibatches, tools/x3_diag.py), which is a discontinuity of the loss, not an accuracy statement.
+Loss statistics to 1e-4 relative.
 """
 import math
 
@@ -51,6 +56,30 @@ def _buffers(pol, M, seed, clip):
     return obs, act.contiguous(), logp_old, adv, ret
 
 
+RELU_MARGIN = 1e-5
+
+
+def _relu_margin(pol, x):
+    """Per row: the smallest |pre-activation| of the hidden layers of both nets, in float64."""
+    x = x.double()
+    ex = pol.mlp_extractor
+    m = torch.full((x.shape[0],), float("inf"), dtype=torch.float64, device=x.device)
+    with torch.no_grad():
+        for net in (ex.policy_net, ex.value_net):
+            h1 = x @ net[0].weight.double().T + net[0].bias.double()
+            h2 = torch.relu(h1) @ net[2].weight.double().T + net[2].bias.double()
+            m = torch.minimum(m, torch.minimum(h1.abs().min(1).values, h2.abs().min(1).values))
+    return m
+
+
+def _index(pol, obs, M, B, seed):
+    """B rows of a seeded permutation of [0, M), skipping rows with an ambiguous ReLU decision."""
+    perm = torch.randperm(M, generator=torch.Generator().manual_seed(seed)).cuda()
+    perm = perm[_relu_margin(pol, obs[perm]) >= RELU_MARGIN]
+    assert perm.numel() >= B
+    return perm[:B].contiguous()
+
+
 def _torch_grads(pol, dtype, obs, act, logp_old, adv, ret, idx, cfg):
     from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
     from uav_reinforcement_learning_control_amd.ppo.ppo import ppo_loss
@@ -63,21 +92,34 @@ def _torch_grads(pol, dtype, obs, act, logp_old, adv, ret, idx, cfg):
     return [p.grad.double() for p in _ordered(ref)], torch.stack([pg, vf, ent, cf]).detach().double()
 
 
+@pytest.fixture(params=["x3", "f32"])
+def learner_form(request, monkeypatch):
+    """Both forms of quad_ppo_grad: k_ppo_grad_x3 (bf16 MFMA on three-piece splits, the default)
+    and k_ppo_grad (f32-input MFMA), selected per call by QUADENV_LEARNER."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    if request.param == "f32":
+        monkeypatch.setenv("QUADENV_LEARNER", "f32")
+    else:
+        monkeypatch.delenv("QUADENV_LEARNER", raising=False)
+    assert N.lib().quad_ppo_grad_form() == (1 if request.param == "x3" else 0)
+    return request.param
+
+
 @pytest.mark.parametrize("M,B,norm,seed", [
-    (6000, 6000, True, 0),       # whole buffer, several blocks with ragged last rounds
+    (6400, 6000, True, 0),       # most of the buffer, several blocks with ragged last rounds
     (20000, 4096 + 17, True, 1),
     (3000, 64, True, 2),         # exactly one round
     (3000, 37, False, 3),        # one partial round, no advantage normalization
     (500, 1, True, 4),           # batch 1: normalization skipped (SB3 len(adv) > 1)
     (300000, 262144, True, 5),   # many rounds per block, the 128-block cap
 ])
-def test_fused_grad_matches_autograd(M, B, norm, seed):
+def test_fused_grad_matches_autograd(M, B, norm, seed, learner_form):
     from uav_reinforcement_learning_control_amd.ppo.learner import FusedLearner, _ordered
     from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig
     cfg = PPOConfig(normalize_advantage=norm)
     pol = _policy(seed)
     obs, act, logp_old, adv, ret = _buffers(pol, M, seed, cfg.clip_range)
-    idx = torch.randperm(M, generator=torch.Generator().manual_seed(seed + 9))[:B].cuda()
+    idx = _index(pol, obs, M, B, seed + 9)
     fl = FusedLearner(pol, cfg.clip_range, cfg.ent_coef, cfg.vf_coef, norm)
     for p in pol.parameters():  # garbage in .grad: the kernel must overwrite, not accumulate
         p.grad = torch.full_like(p, 7.0)
@@ -89,13 +131,15 @@ def test_fused_grad_matches_autograd(M, B, norm, seed):
     ref32, _ = _torch_grads(pol, torch.float32, obs, act, logp_old, adv, ret, idx, cfg)
     names = ["pi_w0", "pi_b0", "pi_w1", "pi_b1", "act_w", "act_b", "vf_w0", "vf_b0", "vf_w1", "vf_b1",
              "val_w", "val_b", "log_std"]
+    bad = []
     for n, g, r64, r32 in zip(names, got, ref64, ref32):
         scale = r64.abs().max().item()
         err = (g - r64).abs().max().item()
         err32 = (r32 - r64).abs().max().item()
         tol = 1e-4 * scale + 4 * err32 + 1e-9  # (long cancelling sums: torch fp32's own error sets the bar)
-        assert err <= tol, f"{n}: max err {err:.3e} > {tol:.3e} (scale {scale:.3e}, torch fp32 err {err32:.3e})"
-        assert err <= 4 * err32 + 1e-6 * scale + 1e-9, f"{n}: err {err:.3e} vs torch fp32 {err32:.3e}"
+        if not (err <= tol and err <= 4 * err32 + 1e-6 * scale + 1e-9):
+            bad.append(f"{n}: max err {err:.3e} (scale {scale:.3e}, torch fp32 err {err32:.3e})")
+    assert not bad, "; ".join(bad)
     np.testing.assert_allclose(stats.double().cpu().numpy(), st64.cpu().numpy(), rtol=1e-4, atol=1e-7)
 
 
@@ -116,7 +160,7 @@ def test_fused_grad_rejects_bad_arguments():
     assert L.quad_ppo_grad(None, None, None, None, 0, None) == N.QUAD_EINVAL
 
 
-def test_ppo_train_fused_matches_torch_update():
+def test_ppo_train_fused_matches_torch_update(learner_form):
     """One PPO.train pass (2 minibatches) with the fused gradient vs the torch loss. Adam's first
     steps move each parameter by ~lr * sign(g), so a gradient element within fp32 noise of zero
     can move either way: allow that (<= 2 lr per step) on a small fraction of the elements, and

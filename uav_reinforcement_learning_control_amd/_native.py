@@ -10,6 +10,8 @@ import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG, "_lib", "libquadenv.so")
+if os.environ.get("QUADENV_LIB"):  # A/B and ablation builds of the same library (tools/*_variants.sh)
+    LIB_PATH = os.environ["QUADENV_LIB"]
 CSRC = os.path.join(_PKG, "csrc")
 
 QUAD_OK, QUAD_EINVAL, QUAD_EHIP, QUAD_ENOMEM, QUAD_EMODEL = 0, -1, -2, -3, -4
@@ -96,7 +98,7 @@ EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_crea
            "quad_kernel_form", "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
            "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
            "quad_waypoints_begin", "quad_waypoints_update", "quad_ppo_workspace_bytes", "quad_ppo_grad",
-           "quad_adam_workspace_bytes", "quad_clip_adam")
+           "quad_ppo_grad_form", "quad_adam_workspace_bytes", "quad_clip_adam")
 
 
 class QuadRollout(C.Structure):
@@ -169,6 +171,8 @@ def _declare(L):
                                         vp, vp, vp, vp, vp]
     L.quad_ppo_workspace_bytes.argtypes = [i32]
     L.quad_ppo_workspace_bytes.restype = C.c_int64
+    L.quad_ppo_grad_form.argtypes = []
+    L.quad_ppo_grad_form.restype = i32
     L.quad_ppo_grad.argtypes = [C.POINTER(QuadPolicyParams), C.POINTER(QuadPPOBatch), C.POINTER(QuadPolicyGrads),
                                 vp, C.c_int64, vp]
     L.quad_adam_workspace_bytes.argtypes = [C.POINTER(QuadAdam)]

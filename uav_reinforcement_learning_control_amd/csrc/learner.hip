@@ -30,8 +30,11 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 
 #include "../../include/quadenv.h"
+#include "learner.h"
 #include "policy_net.h"
 
 namespace quadenv {
@@ -40,14 +43,12 @@ int set_error(int code, const char* msg);  // quadenv.hip
 
 namespace {
 
+using namespace lrn;
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int LB = 256;       // threads per block: 4 waves, one per SIMD
-constexpr int RND = 64;       // rows per round (two 32-row MFMA tiles)
 constexpr int SH = 130;       // row stride (floats) of the [row][neuron] images
 constexpr int SO = 13;        // row stride of the observation image (odd: conflict-free columns)
-constexpr int ADV_BLOCKS = 256;
-constexpr int MAX_NB = 128;   // blocks per net on average (the device has 256 CUs)
 #ifndef QD_LRN_ACTOR_SHARE
 #define QD_LRN_ACTOR_SHARE 540  // measured: 500 -> 1.30 ms, 525 -> 1.26, 540 -> 1.22-1.25, 550 -> 1.23, 580 -> 1.32
 #endif
@@ -64,30 +65,6 @@ constexpr int L_B1 = L_W3T + H * 4, L_B2 = L_B1 + H;
 constexpr int L_TOTAL = L_B2 + H;               // 29,704 floats = 116 KB
 static_assert(L_H1 % 2 == 0 && L_DH2 % 2 == 0 && SH % 2 == 0, "paired reads need 8-byte alignment");
 static_assert(L_W3T % 4 == 0 && L_SC % 4 == 0, "float4 LDS reads");
-
-// per-net partial image (floats): W1 [128][12], b1, W2 [128][128], b2, W3 [NOUT][128], b3,
-// log_std [4] (actor), then 4 statistic slots
-constexpr int P_W1 = 0, P_B1 = P_W1 + H * OBS, P_W2 = P_B1 + H, P_B2 = P_W2 + H * H, P_W3 = P_B2 + H;
-constexpr int P_B3A = P_W3 + ACT * H, P_LS = P_B3A + ACT, P_STATS = P_LS + ACT;  // 18,696
-constexpr int P_B3C = P_W3 + H;
-constexpr int PSTRIDE = P_STATS + 8;   // 18,704 (16-byte multiple)
-static_assert(P_STATS == 18696 && P_B3C + 1 == 18305, "SB3 parameter counts (actor 18,696, critic 18,305)");
-
-struct NetW {
-  const float *w0, *b0, *w1, *b1, *w2, *b2;
-};
-
-struct GArgs {
-  NetW actor, critic;
-  const float* log_std;
-  const float *obs, *act, *logp_old, *adv, *ret;
-  const int64_t* idx;
-  const double* adv_part;  // [ADV_BLOCKS][2] or NULL (no normalization)
-  float* part;             // [nb + nbc][PSTRIDE]: actor blocks, then critic blocks
-  int32_t batch, nb, per_block;     // actor: nb blocks of per_block rows
-  int32_t nbc, per_block_c;         // critic: nbc blocks of per_block_c rows
-  float clip, inv_batch, vf_coef;
-};
 
 // pair-step k order: MFMA step s of lane half h reads neuron 4(s/2) + 2h + (s&1), so two
 // consecutive steps of a lane read two adjacent floats (one ds_read_b64)
@@ -515,29 +492,6 @@ __global__ __launch_bounds__(256) void k_ppo_reduce(RArgs a) {
 
 int lfail(int code, const char* m) { return set_error(code, m); }
 
-struct Layout {
-  int nb, per_block, nbc, per_block_c;
-  int64_t part_bytes, adv_bytes;
-};
-
-Layout layout_of(int32_t batch) {
-  Layout l{};
-  const int rounds = (batch + RND - 1) / RND;
-  // the critic's rows cost less than the actor's (no log-prob / ratio work): the two nets share
-  // the 2 * MAX_NB block slots in proportion to their measured round times (ACTOR_SHARE / 1000)
-  const int slots = rounds < MAX_NB ? 2 * rounds : 2 * MAX_NB;
-  int na = int((int64_t(slots) * ACTOR_SHARE + 500) / 1000);
-  na = na < 1 ? 1 : (na > slots - 1 ? slots - 1 : na);
-  l.nb = na < rounds ? na : rounds;
-  l.nbc = slots - na < rounds ? slots - na : rounds;
-  l.per_block = ((rounds + l.nb - 1) / l.nb) * RND;
-  l.per_block_c = ((rounds + l.nbc - 1) / l.nbc) * RND;
-  l.part_bytes = int64_t(l.nb + l.nbc) * PSTRIDE * int64_t(sizeof(float));
-  l.adv_bytes = int64_t(ADV_BLOCKS) * 2 * int64_t(sizeof(double));
-  return l;
-}
-
-
 // ---- fused clip_grad_norm_ + Adam (quad_clip_adam)
 constexpr int ADAM_BLOCK = 256;
 
@@ -625,13 +579,21 @@ int adam_layout(const QuadAdam* a, AdamArgs& g) {
 }  // namespace quadenv
 
 using namespace quadenv;
+using namespace quadenv::lrn;
 
 extern "C" {
 
 int64_t quad_ppo_workspace_bytes(int32_t batch) {
   if (batch < 1) return 0;
-  const Layout l = layout_of(batch);
+  const Layout l = layout_of(batch, ACTOR_SHARE);  // the partial image is sized for every split
   return l.adv_bytes + l.part_bytes;
+}
+
+// 1: the bf16x3 form (k_ppo_grad_x3, default), 0: the f32-input MFMA form (k_ppo_grad);
+// QUADENV_LEARNER=f32 selects the latter (read per call, so a process can A/B both)
+int quad_ppo_grad_form(void) {
+  const char* v = std::getenv("QUADENV_LEARNER");
+  return (v && std::strcmp(v, "f32") == 0) ? 0 : 1;
 }
 
 int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPolicyGrads* gr, void* workspace,
@@ -650,13 +612,14 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
     return lfail(QUAD_EINVAL, "obs and actions must be 16-byte aligned");
   if (reinterpret_cast<uintptr_t>(workspace) & 15u) return lfail(QUAD_EINVAL, "workspace must be 16-byte aligned");
   if (!(b->clip_range > 0.f)) return lfail(QUAD_EINVAL, "clip_range must be > 0");
-  const Layout l = layout_of(b->batch);
+  const bool x3 = quad_ppo_grad_form() == 1;
+  const Layout l = layout_of(b->batch, x3 ? x3_actor_share() : ACTOR_SHARE);
   if (workspace_bytes < l.adv_bytes + l.part_bytes) return lfail(QUAD_EINVAL, "workspace too small");
   static bool opted[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return lfail(QUAD_EHIP, "hipGetDevice failed");
   const int lds_bytes = L_TOTAL * int(sizeof(float));
-  if (!opted[dev]) {
+  if (!x3 && !opted[dev]) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad), hipFuncAttributeMaxDynamicSharedMemorySize,
                             lds_bytes) != hipSuccess)
       return lfail(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
@@ -680,8 +643,12 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   g.part = part;
   g.batch = b->batch; g.nb = l.nb; g.per_block = l.per_block; g.nbc = l.nbc; g.per_block_c = l.per_block_c;
   g.clip = b->clip_range; g.inv_batch = 1.0f / float(b->batch); g.vf_coef = b->vf_coef;
-  hipLaunchKernelGGL(k_ppo_grad, dim3(l.nb + l.nbc), dim3(LB), lds_bytes, s, g);
-  if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_grad launch failed");
+  if (x3) {
+    if (int rc = launch_ppo_grad_x3(g, s)) return rc;
+  } else {
+    hipLaunchKernelGGL(k_ppo_grad, dim3(l.nb + l.nbc), dim3(LB), lds_bytes, s, g);
+    if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_grad launch failed");
+  }
   RArgs r{};
   r.gr = *gr; r.part = part; r.log_std = p->log_std; r.stats = b->stats; r.nb = l.nb; r.nbc = l.nbc;
   r.inv_batch = 1.0f / float(b->batch); r.ent_coef = b->ent_coef;

@@ -1,0 +1,641 @@
+// learner_x3.hip -- the PPO minibatch gradient (row P) on bf16 MFMA with three-piece splits
+// (k_ppo_grad_x3): f32 accuracy at the bf16 matrix rate.
+//
+// Every f32 operand x of the three 128-deep products (L2, dW2, dh1) and of L1 / dW1 is split into
+// three bf16 pieces x = x0 + x1 + x2, each the round-to-nearest bf16 of what the previous pieces
+// leave (exact: x0 takes the top 8 significant bits, the f32 residual x - x0 has at most 16, the
+// second residual at most 8, so the three pieces hold x exactly outside the subnormal range). A
+// product a*b is formed as the six MFMAs a2b0 + a1b1 + a0b2 + a1b0 + a0b1 + a0b0 accumulated in f32
+// (v_mfma_f32_32x32x16_bf16: exact bf16 products, f32 sums); the dropped a1b2 + a2b1 + a2b2 are
+// <= ~2^-23 |ab|, one f32 rounding of the product. So each K-step of 16 costs 6 x 32 cycles instead
+// of 8 x 64 cycles of v_mfma_f32_32x32x2_f32 (2.7x less matrix time) at f32-level error; the
+// accuracy bar is the same as the f32 form's (tests/test_gpu_learner.py, both forms).
+//
+// Structure (per block: one net, 4 waves, wave w owns neurons 32w..32w+31 of both hidden layers,
+// rounds of 64 minibatch rows = two 32-row tiles; the loss math is learner.hip's):
+//   L1   h1^T = W1 x^T        E form (neurons in registers, rows on lanes)  -> H1 pieces image
+//   L2   h2^T = W2 h1^T       E form: A = W2 rows (registers), B = H1 row reads (ds_read_b128)
+//   head / loss / dL/dmean    VALU, as learner.hip
+//   dh2  E form               -> DH2 pieces image, relu(h2) -> f32 image (dW3), db2 per lane
+//   dW2  = dh2^T h1 (K = rows)  A = DH2, B = H1, both by transposed reads (ds_read_b64_tr_b16)
+//   dW3  = dmean^T h2         f32 16x16x4 MFMA (small)
+//   dh1  R form (rows in registers): A = DH2 row reads, B = W2 columns (registers); relu'(h1)
+//        from the H1 image by transposed reads
+//   dW1  = dh1^T x            the dh1 accumulator split in registers is the A operand; B = the
+//        observation image by transposed reads; its column 12 is 1.0, so dW1's column 12 is db1
+// The [64 row][128 neuron] bf16 images have 272-byte rows (see soff).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+
+#include "../../include/quadenv.h"
+#include "learner.h"
+
+namespace quadenv {
+
+int set_error(int code, const char* msg);  // quadenv.hip
+
+namespace lrn {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+struct X3 {
+  bf16x8 p[3];  // x = p[0] + p[1] + p[2]
+};
+struct X3h {
+  bf16x4 p[3];
+};
+
+// LDS (bytes)
+constexpr int RS = 272;                        // row stride (bytes) of the bf16 images: 256 + 16
+constexpr int IMG = RND * RS;                  // one [64 row][128 neuron] bf16 piece
+constexpr int SH = 130;                        // row stride (floats) of the f32 relu(h2) image
+constexpr int XROW = 32;                       // observation image row: 12 features, 1.0, 3 zeros (bf16)
+constexpr int XIMG = RND * XROW;
+constexpr int B_H1P = 0;                       // 3 pieces
+constexpr int B_DH2P = B_H1P + 3 * IMG;        // 3 pieces
+constexpr int B_H2 = B_DH2P + 3 * IMG;         // f32 [64][SH]
+constexpr int B_XO = B_H2 + RND * SH * 4;      // [2 round buffers][3 pieces][64][16] bf16
+constexpr int B_ZERO = B_XO + 2 * 3 * XIMG;    // 64 zero bytes: dW1's padded columns 16..31
+constexpr int B_SC = B_ZERO + 64;              // f32 [2][64][8] row scalars: action 4, old logp, adv, return
+constexpr int B_DM = B_SC + 2 * RND * 8 * 4;   // f32 [64][4] dL/dmean (dL/dV in column 0)
+constexpr int B_PART = B_DM + RND * 16;        // f32 [4 waves][64][4] head partial sums
+constexpr int B_W3T = B_PART + 4 * RND * 16;   // f32 [128][4] head weights, neuron-major
+constexpr int B_B1 = B_W3T + H * 16, B_B2 = B_B1 + H * 4;
+constexpr int B_TOTAL = B_B2 + H * 4;          // 162,368 B
+static_assert(B_TOTAL <= 160 * 1024, "LDS budget");
+static_assert(B_XO % 16 == 0 && B_SC % 16 == 0 && B_W3T % 16 == 0 && B_H2 % 16 == 0, "alignment");
+static_assert(2 * LB * 8 <= RND * SH * 4, "the advantage reduction aliases the relu(h2) image");
+
+// byte offset of 16-byte chunk `ch` of image row `row`. Padded rows (68 dwords) instead of an XOR
+// swizzle: every address is affine in the k-step / tile / block indices, so each read takes one
+// base register and an immediate offset (the XOR form held ~100 hoisted address VGPRs, and spilled);
+// the 16-byte row reads are conflict-free, the 4-row transposed reads 2-way.
+// scheduling fence between k-steps (bounds how far the compiler hoists operand reads)
+#if defined(QD_X3_NOSB)
+#define X3_SB() ((void)0)
+#else
+#define X3_SB() __builtin_amdgcn_sched_barrier(0)
+#endif
+
+__device__ __forceinline__ int soff(int row, int ch) { return RS * row + 16 * ch; }
+
+// three-piece split of two floats (exact residuals: x - bf16(x) is representable in f32)
+__device__ __forceinline__ void split2(float a, float b, bf16x2& p0, bf16x2& p1, bf16x2& p2) {
+  const f32x2 x = {a, b};
+  p0 = __builtin_convertvector(x, bf16x2);
+  const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
+  p1 = __builtin_convertvector(r1, bf16x2);
+  const f32x2 r2 = r1 - __builtin_convertvector(p1, f32x2);
+  p2 = __builtin_convertvector(r2, bf16x2);
+}
+
+__device__ __forceinline__ X3h split4(const float (&v)[4]) {
+  bf16x2 a0, a1, a2, b0, b1, b2;
+  split2(v[0], v[1], a0, a1, a2);
+  split2(v[2], v[3], b0, b1, b2);
+  X3h o;
+  o.p[0] = __builtin_shufflevector(a0, b0, 0, 1, 2, 3);
+  o.p[1] = __builtin_shufflevector(a1, b1, 0, 1, 2, 3);
+  o.p[2] = __builtin_shufflevector(a2, b2, 0, 1, 2, 3);
+  return o;
+}
+
+__device__ __forceinline__ X3 split8(const float (&v)[8]) {
+  const float lo[4] = {v[0], v[1], v[2], v[3]}, hi[4] = {v[4], v[5], v[6], v[7]};
+  const X3h a = split4(lo), b = split4(hi);
+  X3 o;
+#pragma unroll
+  for (int p = 0; p < 3; p++) o.p[p] = __builtin_shufflevector(a.p[p], b.p[p], 0, 1, 2, 3, 4, 5, 6, 7);
+  return o;
+}
+
+__device__ __forceinline__ f32x16 mfma16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// a*b over one K-step of 16 at f32 accuracy (small terms first)
+__device__ __forceinline__ f32x16 mma3(const X3& a, const X3& b, f32x16 c) {
+  c = mfma16(a.p[2], b.p[0], c);
+  c = mfma16(a.p[1], b.p[1], c);
+  c = mfma16(a.p[0], b.p[2], c);
+  c = mfma16(a.p[1], b.p[0], c);
+  c = mfma16(a.p[0], b.p[1], c);
+  return mfma16(a.p[0], b.p[0], c);
+}
+
+__device__ __forceinline__ bf16x8 rd16(const char* L, int off) { return *reinterpret_cast<const bf16x8*>(L + off); }
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q / columns 4p..4p+3 of a 4 x 16
+// block; lane i receives column i of the 4 rows (row q in element q)
+__device__ __forceinline__ s16x4 rdtr(const char* L, int off) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(L + off));
+}
+
+__device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
+  return __builtin_bit_cast(bf16x8, s16x8(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)));
+}
+
+template <int NOUT>
+__device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int blk) {
+  const NetW& W = NOUT == ACT ? g.actor : g.critic;
+  float* const Lf = reinterpret_cast<float*>(L);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int n_own = 32 * w + l32;
+  // transposed-read roles: lane 4 gq + gp of its 16-lane group; ghi = which 16 columns of a 32-block
+  const int gq = (lane & 15) >> 2, gp = lane & 3, ghi = (lane >> 4) & 1;
+  const int tr_col = 2 * ghi + (gp >> 1), tr_half = 8 * (gp & 1);
+
+  // ---- advantage statistics of the minibatch (actor): fixed-order tree over the pre-pass partials
+  float adv_mu = 0.f, adv_den = 1.f;
+  if (NOUT == ACT && g.adv_part) {
+    double* red = reinterpret_cast<double*>(L + B_H2);  // [2][LB], before the relu(h2) image is used
+    red[tid] = g.adv_part[2 * tid];
+    red[LB + tid] = g.adv_part[2 * tid + 1];
+    __syncthreads();
+    for (int o = LB / 2; o > 0; o >>= 1) {
+      if (tid < o) { red[tid] += red[tid + o]; red[LB + tid] += red[LB + tid + o]; }
+      __syncthreads();
+    }
+    const double n = double(g.batch), s = red[0], s2 = red[LB];
+    const double var = fmax((s2 - s * s / n) / (n - 1.0), 0.0);
+    adv_mu = float(s / n);
+    adv_den = float(sqrt(var)) + 1e-8f;
+  }
+
+  // ---- small weights in LDS; the wave's W1 / W2 fragments split in registers
+  for (int i = tid; i < H; i += LB) {
+    Lf[B_B1 / 4 + i] = W.b0[i];
+    Lf[B_B2 / 4 + i] = W.b1[i];
+#pragma unroll
+    for (int k = 0; k < 4; k++) Lf[B_W3T / 4 + 4 * i + k] = k < NOUT ? W.w2[k * H + i] : 0.f;
+  }
+  if (tid < 16) Lf[B_ZERO / 4 + tid] = 0.f;
+  float b3[NOUT];
+#pragma unroll
+  for (int k = 0; k < NOUT; k++) b3[k] = W.b2[k];
+  X3 w1x;  // A of L1: W1[n_own][f = 8h + j] (f >= 12: 0)
+  {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = 8 * h + j < OBS ? W.w0[n_own * OBS + 8 * h + j] : 0.f;
+    w1x = split8(v);
+  }
+  // W2 slices in f32, split into pieces at each use (the split pieces of both would take 192 VGPRs).
+  // k order of the 128-deep products: at k-step s, lane half h holds k = 8s + 64h + j, i.e. chunk
+  // s + 8h of an image row, so lanes l and l + 32 read chunks 128 B apart (conflict-free b128 reads):
+  // wA[s][j] = W2[n_own][kk] (A of L2), wB[s][j] = W2[kk][n_own] (B of dh1), kk = 8s + 64h + j
+  float wA[8][8], wB[8][8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      wA[s][j] = W.w1[n_own * H + 8 * s + 64 * h + j];
+      wB[s][j] = W.w1[(8 * s + 64 * h + j) * H + n_own];
+    }
+  }
+#if defined(QD_X3_PRESPLIT_A)
+  X3 wAx[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) wAx[s] = split8(wA[s]);
+#define SPLIT_A(s) wAx[s]
+#else
+#define SPLIT_A(s) split8(wA[s])
+#endif
+#if defined(QD_X3_PRESPLIT_B)
+  X3 wBx[8];
+#pragma unroll
+  for (int s = 0; s < 8; s++) wBx[s] = split8(wB[s]);
+#define SPLIT_B(s) wBx[s]
+#else
+#define SPLIT_B(s) split8(wB[s])
+#endif
+  float ls[ACT], sd[ACT];
+  if constexpr (NOUT == ACT) {
+#pragma unroll
+    for (int k = 0; k < ACT; k++) { ls[k] = g.log_std[k]; sd[k] = expf(ls[k]); }
+  }
+
+  // accumulators (whole launch)
+  f32x16 dW2[4], dW1;
+  f32x4 dW3[2], dM[2];  // dM[o][n] = sum_rows dL/dmean[row][o] relu'(h2[row][n]): db2 = sum_o W3[o][n] dM[o][n]
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    dW1[r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) dW2[j][r] = 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) { dW3[0][r] = 0.f; dW3[1][r] = 0.f; dM[0][r] = 0.f; dM[1][r] = 0.f; }
+  float db3[NOUT], dls[ACT], st[3] = {0.f, 0.f, 0.f};  // st: pg sum, vf sum, clipped count
+#pragma unroll
+  for (int k = 0; k < NOUT; k++) db3[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < ACT; k++) dls[k] = 0.f;
+  const bool acc_lane = w == 0 && h == 0;  // one lane per row accumulates the per-row sums
+
+  const int per_block = NOUT == ACT ? g.per_block : g.per_block_c;
+  const int s0 = blk * per_block;
+  const int s1 = min(g.batch, s0 + per_block);
+  const int rounds = s1 > s0 ? (s1 - s0 + RND - 1) / RND : 0;
+  // Row staging, one round ahead: threads 0..191 gather the observation rows (float4 each),
+  // threads 192..255 the row scalars; the minibatch indices are loaded two rounds ahead.
+  const int srow = tid < 3 * RND ? tid / 3 : tid - 3 * RND;
+  auto index_of = [&](int rd) -> int64_t {
+    const int i = s0 + rd * RND + srow;
+    return (rd < rounds && i < s1) ? g.idx[i] : int64_t(-1);
+  };
+  float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
+  float pfs[3] = {0.f, 0.f, 0.f};
+  auto gather = [&](int64_t row) {
+    pf = make_float4(0.f, 0.f, 0.f, 0.f);
+    pfs[0] = pfs[1] = pfs[2] = 0.f;
+    if (row < 0) return;
+    if (tid < 3 * RND) {
+      pf = reinterpret_cast<const float4*>(g.obs)[size_t(row) * 3 + tid % 3];
+    } else if (NOUT == ACT) {
+      pf = reinterpret_cast<const float4*>(g.act)[row];
+      pfs[0] = g.logp_old[row];
+      pfs[1] = g.adv[row];
+    } else {
+      pfs[2] = g.ret[row];
+    }
+  };
+  gather(index_of(0));
+  int64_t next_row = index_of(1);
+  __syncthreads();
+
+  for (int rd = 0; rd < rounds; rd++) {
+    const int base = s0 + rd * RND;
+    char* const XO = L + B_XO + (rd & 1) * 3 * XIMG;
+    float* const SCI = Lf + B_SC / 4 + (rd & 1) * RND * 8;
+    if (tid < 3 * RND) {
+      const float v[4] = {pf.x, pf.y, pf.z, pf.w};
+      const X3h x = split4(v);
+      const int c = tid % 3;
+#pragma unroll
+      for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(XO + p * XIMG + srow * XROW + 8 * c) = x.p[p];
+      if (c == 2) {  // features 12..15: 1.0 (dW1's column 12 is db1), 0, 0, 0
+        const bf16x4 one = {__bf16(1.f), __bf16(0.f), __bf16(0.f), __bf16(0.f)}, zero = {};
+        *reinterpret_cast<bf16x4*>(XO + srow * XROW + 24) = one;
+        *reinterpret_cast<bf16x4*>(XO + XIMG + srow * XROW + 24) = zero;
+        *reinterpret_cast<bf16x4*>(XO + 2 * XIMG + srow * XROW + 24) = zero;
+      }
+    } else {
+      *reinterpret_cast<float4*>(SCI + srow * 8) = pf;
+      SCI[srow * 8 + 4] = pfs[0]; SCI[srow * 8 + 5] = pfs[1]; SCI[srow * 8 + 6] = pfs[2];
+    }
+    gather(next_row);           // round rd + 1, in flight during this round
+    next_row = index_of(rd + 2);
+    bool valid[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) valid[t] = base + 32 * t + l32 < s1;
+    __syncthreads();  // B1: observation image complete; the previous round's readers are done
+
+    // ---- L1 (E form): h1^T block w of both tiles -> H1 pieces
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      f32x16 acc;
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[r] = Lf[B_B1 / 4 + 32 * w + acc_row(r, h)];
+      X3 xb;
+#pragma unroll
+      for (int p = 0; p < 3; p++) xb.p[p] = rd16(XO, p * XIMG + (32 * t + l32) * XROW + 16 * h);
+      acc = mma3(w1x, xb, acc);
+#pragma unroll
+      for (int gg = 0; gg < 4; gg++) {  // registers 4gg.. = neurons 32w + 8gg + 4h + 0..3
+        const float v[4] = {fmaxf(acc[4 * gg], 0.f), fmaxf(acc[4 * gg + 1], 0.f), fmaxf(acc[4 * gg + 2], 0.f),
+                            fmaxf(acc[4 * gg + 3], 0.f)};
+        const X3h x = split4(v);
+        const int off = soff(32 * t + l32, 4 * w + gg) + 8 * h;
+#pragma unroll
+        for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_H1P + p * IMG + off) = x.p[p];
+      }
+    }
+    __syncthreads();  // B2: H1 image complete
+
+#if !defined(QD_X3_NOL2)
+    // ---- L2 (E form): h2^T block w, A = W2 rows (registers), B = H1 row reads
+    f32x16 h2[2];
+#pragma unroll
+    for (int r = 0; r < 16; r++) h2[0][r] = Lf[B_B2 / 4 + 32 * w + acc_row(r, h)];
+    h2[1] = h2[0];
+    {  // software pipeline: step s's MFMAs with step s + 1's reads and weight split in flight
+      X3 a = SPLIT_A(0), b[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int p = 0; p < 3; p++) b[t].p[p] = rd16(L, B_H1P + p * IMG + soff(32 * t + l32, 8 * h));
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        X3 an, bn[2];
+        if (s < 7) {
+#pragma unroll
+          for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int p = 0; p < 3; p++) bn[t].p[p] = rd16(L, B_H1P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
+          an = SPLIT_A(s + 1);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; t++) h2[t] = mma3(a, b[t], h2[t]);
+        X3_SB();
+        if (s < 7) { a = an; b[0] = bn[0]; b[1] = bn[1]; }
+      }
+    }
+#else
+    f32x16 h2[2];
+    for (int r = 0; r < 16; r++) { h2[0][r] = Lf[r]; h2[1][r] = Lf[r + 16]; }
+#endif
+    // head partial sums over the wave's 32 neurons (the two lane halves hold 16 each)
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      float part[NOUT];
+#pragma unroll
+      for (int k = 0; k < NOUT; k++) part[k] = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        h2[t][r] = fmaxf(h2[t][r], 0.f);
+        const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * (32 * w + acc_row(r, h)));
+        const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
+#pragma unroll
+        for (int k = 0; k < NOUT; k++) part[k] = fmaf(wk[k], h2[t][r], part[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < NOUT; k++) {
+        const float o = __shfl_xor(part[k], 32);
+        if (h == 0) Lf[B_PART / 4 + (w * RND + 32 * t + l32) * 4 + k] = part[k] + o;
+      }
+    }
+    __syncthreads();  // B3: head partials complete
+
+    // ---- per-row loss terms and dL/d(head output) (every wave, identical arithmetic)
+    float d[2][NOUT];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const int e = 32 * t + l32;
+      const float* PT = Lf + B_PART / 4;
+      float out[NOUT];
+#pragma unroll
+      for (int k = 0; k < NOUT; k++)
+        out[k] = (((PT[e * 4 + k] + PT[(RND + e) * 4 + k]) + PT[(2 * RND + e) * 4 + k]) + PT[(3 * RND + e) * 4 + k]) +
+                 b3[k];
+      const float4 a4 = *reinterpret_cast<const float4*>(SCI + e * 8);
+      const float a4k[4] = {a4.x, a4.y, a4.z, a4.w};
+      if constexpr (NOUT == ACT) {
+        float z[ACT], lp = 0.f;
+#pragma unroll
+        for (int k = 0; k < ACT; k++) {
+          z[k] = (a4k[k] - out[k]) / sd[k];
+          lp += -0.5f * z[k] * z[k] - ls[k] - 0.91893853320467274f;
+        }
+        const float r = expf(lp - SCI[e * 8 + 4]);
+        const float A = g.adv_part ? (SCI[e * 8 + 5] - adv_mu) / adv_den : SCI[e * 8 + 5];
+        const float cr = fminf(fmaxf(r, 1.f - g.clip), 1.f + g.clip);
+        const float sa = A * r, sb = A * cr;
+        const float w1 = sa < sb ? 1.f : (sa == sb ? 0.5f : 0.f);
+        const float inr = (r >= 1.f - g.clip && r <= 1.f + g.clip) ? 1.f : 0.f;
+        const float dlp = valid[t] ? -g.inv_batch * A * (w1 + (1.f - w1) * inr) * r : 0.f;
+#pragma unroll
+        for (int k = 0; k < ACT; k++) d[t][k] = dlp * z[k] / sd[k];
+        if (acc_lane && valid[t]) {
+          st[0] += -fminf(sa, sb);
+          st[2] += fabsf(r - 1.f) > g.clip ? 1.f : 0.f;
+#pragma unroll
+          for (int k = 0; k < ACT; k++) dls[k] += dlp * (z[k] * z[k] - 1.f);
+        }
+      } else {
+        const float diff = out[0] - SCI[e * 8 + 6];
+        d[t][0] = valid[t] ? 2.f * g.vf_coef * g.inv_batch * diff : 0.f;
+        if (acc_lane && valid[t]) st[1] += diff * diff;
+      }
+      if (acc_lane) {
+#pragma unroll
+        for (int k = 0; k < NOUT; k++) {
+          db3[k] += d[t][k];
+          Lf[B_DM / 4 + e * 4 + k] = d[t][k];
+        }
+      }
+    }
+    // ---- dh2 (E form) -> DH2 pieces; relu(h2) -> f32 image; db2 per lane
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      float* rowh = Lf + B_H2 / 4 + (32 * t + l32) * SH + 32 * w;
+#pragma unroll
+      for (int gg = 0; gg < 4; gg++) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int r = 4 * gg + u;
+          const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * (32 * w + acc_row(r, h)));
+          const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
+          float gsum = 0.f;
+#pragma unroll
+          for (int k = 0; k < NOUT; k++) gsum = fmaf(wk[k], d[t][k], gsum);
+          v[u] = h2[t][r] > 0.f ? gsum : 0.f;
+        }
+        const X3h x = split4(v);
+        const int off = soff(32 * t + l32, 4 * w + gg) + 8 * h;
+#pragma unroll
+        for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_DH2P + p * IMG + off) = x.p[p];
+        *reinterpret_cast<float2*>(rowh + 8 * gg + 4 * h) = make_float2(h2[t][4 * gg], h2[t][4 * gg + 1]);
+        *reinterpret_cast<float2*>(rowh + 8 * gg + 4 * h + 2) = make_float2(h2[t][4 * gg + 2], h2[t][4 * gg + 3]);
+      }
+    }
+    __syncthreads();  // B4: DH2, relu(h2) and dL/dmean images complete
+
+#if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
+    // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
+    {  // 20 operand blocks (per k-step s: A, then B of jb = 0..3), each read one unit ahead
+      auto trblk = [&](int img, int s, int chunk) {
+        const int r0 = 16 * s + 8 * h + gq;
+        X3 x;
+#pragma unroll
+        for (int p = 0; p < 3; p++) {
+          const char* I = L + img + p * IMG;
+          x.p[p] = cat_tr(rdtr(I, soff(r0, chunk) + tr_half), rdtr(I, soff(r0 + 4, chunk) + tr_half));
+        }
+        return x;
+      };
+      X3 a = trblk(B_DH2P, 0, 4 * w + tr_col), b = trblk(B_H1P, 0, tr_col);
+#pragma unroll
+      for (int s = 0; s < 4; s++) {
+#pragma unroll
+        for (int jb = 0; jb < 4; jb++) {
+          X3 an, bn;
+          if (jb < 3) bn = trblk(B_H1P, s, 4 * (jb + 1) + tr_col);
+          else if (s < 3) { an = trblk(B_DH2P, s + 1, 4 * w + tr_col); bn = trblk(B_H1P, s + 1, tr_col); }
+          dW2[jb] = mma3(a, b, dW2[jb]);
+          X3_SB();
+          if (jb < 3) b = bn;
+          else if (s < 3) { a = an; b = bn; }
+        }
+      }
+    }
+#endif
+    // ---- dW3 columns 32w.. (f32 16x16x4: A = dL/dmean^T (rows = outputs), B = relu(h2) rows)
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+      const int e = 4 * s + (lane >> 4), k = lane & 15;
+      const float a = k < NOUT ? Lf[B_DM / 4 + e * 4 + k] : 0.f;
+#pragma unroll
+      for (int b = 0; b < 2; b++) {
+        const float hv = Lf[B_H2 / 4 + e * SH + 32 * w + 16 * b + k];
+        dW3[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, hv, dW3[b], 0, 0, 0);
+        dM[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, hv > 0.f ? 1.f : 0.f, dM[b], 0, 0, 0);
+      }
+    }
+#if !defined(QD_X3_NODH1)
+    // ---- dh1 (R form) = relu'(h1) . (dh2 W2[:, block w]); then the dW1 slab (+ db1 in column 12)
+    f32x16 dh1[2];
+#pragma unroll
+    for (int r = 0; r < 16; r++) { dh1[0][r] = 0.f; dh1[1][r] = 0.f; }
+    {  // software pipeline as L2: A = DH2 row reads, B = split W2 columns
+      X3 b = SPLIT_B(0), a[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int p = 0; p < 3; p++) a[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, 8 * h));
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        X3 bn, an[2];
+        if (s < 7) {
+#pragma unroll
+          for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int p = 0; p < 3; p++) an[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
+          bn = SPLIT_B(s + 1);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; t++) dh1[t] = mma3(a[t], b, dh1[t]);
+        X3_SB();
+        if (s < 7) { b = bn; a[0] = an[0]; a[1] = an[1]; }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      f32x16& acc = dh1[t];
+      // register r: row 32t + acc_row(r, h), neuron n_own; relu'(h1) from the top piece of h1
+      // (h1 >= 0 after the ReLU: its top piece is > 0 exactly when h1 is a positive normal)
+#pragma unroll
+      for (int gg = 0; gg < 4; gg++) {
+        const s16x4 m = rdtr(L + B_H1P, soff(32 * t + 8 * gg + 4 * h + gq, 4 * w + tr_col) + tr_half);
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[4 * gg + q] = m[q] > 0 ? acc[4 * gg + q] : 0.f;
+      }
+      // dW1[n][f] += sum_rows dh1[row][n] x[row][f]: registers 8s2.. are the A^T fragment of k-step
+      // s2, rows 32t + 16 s2 + 8(j >> 2) + 4h + (j & 3); B from the observation image (zeros past f 15)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; s2++) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = acc[8 * s2 + j];
+        const X3 a = split8(v);
+        const int rr = 32 * t + 16 * s2 + 4 * h + gq;
+        X3 b;
+#pragma unroll
+        for (int p = 0; p < 3; p++) {
+          const int o0 = ghi ? B_ZERO - B_XO - (rd & 1) * 3 * XIMG + 8 * gp : p * XIMG + rr * XROW + 8 * gp;
+          const int o1 = ghi ? o0 : o0 + 8 * XROW;
+          b.p[p] = cat_tr(rdtr(XO, o0), rdtr(XO, o1));
+        }
+        dW1 = mma3(a, b, dW1);
+      }
+    }
+  #endif
+}
+
+  // ---- block partials in the parameter layout
+  float* P = g.part + size_t(blk + (NOUT == ACT ? 0 : g.nb)) * PSTRIDE;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int n = 32 * w + acc_row(r, h);
+    if (l32 < OBS) P[P_W1 + n * OBS + l32] = dW1[r];
+    if (l32 == OBS) P[P_B1 + n] = dW1[r];
+#pragma unroll
+    for (int j = 0; j < 4; j++) P[P_W2 + n * H + 32 * j + l32] = dW2[j][r];
+  }
+  if (lane < 16) {  // rows o < 4 of the 16x16 outputs: lanes 0..15, register o
+#pragma unroll
+    for (int b = 0; b < 2; b++) {
+      const int n = 32 * w + 16 * b + lane;
+      const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * n);
+      const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
+      float db2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < NOUT; r++) {
+        P[P_W3 + r * H + n] = dW3[b][r];
+        db2 = fmaf(wk[r], dM[b][r], db2);
+      }
+      P[P_B2 + n] = db2;
+    }
+  }
+  if (w == 0) {  // lanes 0..31 hold the per-row sums (lanes 32..63 hold zeros)
+    float v[NOUT + ACT + 3];
+    int nv = 0;
+#pragma unroll
+    for (int k = 0; k < NOUT; k++) v[nv++] = db3[k];
+#pragma unroll
+    for (int k = 0; k < ACT; k++) v[nv++] = dls[k];
+#pragma unroll
+    for (int k = 0; k < 3; k++) v[nv++] = st[k];
+#pragma unroll
+    for (int q = 0; q < NOUT + ACT + 3; q++) {
+      float x = v[q];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      v[q] = x;
+    }
+    if (lane == 0) {
+      const int b3off = NOUT == ACT ? P_B3A : P_B3C;
+#pragma unroll
+      for (int k = 0; k < NOUT; k++) P[b3off + k] = v[k];
+      if (NOUT == ACT) {
+#pragma unroll
+        for (int k = 0; k < ACT; k++) P[P_LS + k] = v[NOUT + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; k++) P[P_STATS + k] = v[NOUT + ACT + k];
+    }
+  }
+}
+
+__global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3(GArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds_x3[];
+  if (int(blockIdx.x) < g.nb) body<ACT>(g, lds_x3, blockIdx.x);
+  else body<1>(g, lds_x3, blockIdx.x - g.nb);
+}
+
+}  // namespace
+
+#ifndef QD_LRN_X3_ACTOR_SHARE
+#define QD_LRN_X3_ACTOR_SHARE 540
+#endif
+int x3_actor_share() { return QD_LRN_X3_ACTOR_SHARE; }
+
+int launch_ppo_grad_x3(const GArgs& g, hipStream_t s) {
+  static bool opted[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return set_error(QUAD_EHIP, "hipGetDevice failed");
+  if (!opted[dev]) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_x3), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            B_TOTAL) != hipSuccess)
+      return set_error(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    opted[dev] = true;
+  }
+  hipLaunchKernelGGL(k_ppo_grad_x3, dim3(g.nb + g.nbc), dim3(LB), B_TOTAL, s, g);
+  if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3 launch failed");
+  return QUAD_OK;
+}
+
+}  // namespace lrn
+}  // namespace quadenv
