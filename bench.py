@@ -276,12 +276,26 @@ def _learner_kernel(m) -> dict:
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
-    # issued MFMA work per row per net: (12 + 128 + 128 + 128 + 32) 32x32x2 per 64 rows per wave x 4
-    # waves, plus 32 16x16x4 (half the cycles) -> 444 x 2048 x 2 flop x 4 / 64 rows
+    # the f32 algorithm's MFMA work per row per net: (12 + 128 + 128 + 128 + 32) 32x32x2 per 64 rows
+    # per wave x 4 waves, plus 32 16x16x4 (half the cycles) -> 444 x 2048 x 2 flop x 4 / 64 rows
     flop = 2 * m.batch * (444 * 2048 * 2 * 4 / 64)
-    return {"kernel": "quad_ppo_grad (k_adv_stats + k_ppo_grad + k_ppo_reduce)", "rows": m.batch,
-            "us_per_minibatch": us, "issued_flop": flop, "achieved_TFLOPs": flop / us / 1e6,
-            "peak_TFLOPs": 157.3, "bound": "mfma (fp32 32x32x2)"}
+    from uav_reinforcement_learning_control_amd import _native as N
+    form = int(N.lib().quad_ppo_grad_form())
+    out = {"kernel": "quad_ppo_grad (k_adv_stats + %s + k_ppo_reduce)" % ("k_ppo_grad_x3" if form else "k_ppo_grad"),
+           "rows": m.batch, "us_per_minibatch": us, "issued_flop": flop}
+    if form:
+        # bf16x3: per 64-row round and wave 324 v_mfma_f32_32x32x16_bf16 (32 cycles each: L1 12, L2 96,
+        # dW2 96, dh1 96, dW1 24) + 64 f32 16x16x4 (dW3 and the db2 mask sums, 32 cycles each)
+        cyc = 2 * (m.batch / 64) * 4 * (324 * 32 + 64 * 32) / 1024  # per SIMD, both nets
+        floor_us = cyc / 2.4e3  # at the 2.4 GHz peak clock
+        out.update({"f32_equivalent_TFLOPs": flop / us / 1e6, "peak_TFLOPs": 157.3,
+                    "f32_equivalent_frac": flop / us / 1e6 / 157.3,
+                    "bound": "mfma (bf16 32x32x16 on three-piece splits: f32-level error)",
+                    "matrix_pipe_floor_us": floor_us, "matrix_pipe_frac": floor_us / us,
+                    "achieved_TFLOPs": flop / us / 1e6})
+    else:
+        out.update({"achieved_TFLOPs": flop / us / 1e6, "peak_TFLOPs": 157.3, "bound": "mfma (fp32 32x32x2)"})
+    return out
 
 
 def _rollout_phase(env, args) -> dict:
