@@ -14,10 +14,11 @@ run() {  # name timeout cmd...
   echo "=== $name rc=$rc"; tail -n 3 "gpurun_out/$name.log"
   if [ $rc -ne 0 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
 }
-STEPS=${STEPS:-pytest,smoke,bench,prof,pmc}
+STEPS=${STEPS:-pytest,smoke,bench,prof,pmc,lrnpmc}
 [[ $STEPS == *pytest* ]] && run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 [[ $STEPS == *smoke* ]] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
 [[ $STEPS == *prof* ]] && run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --e2e-iters 0
-[[ $STEPS == *pmc* ]] && run pmc 900 bash tools/pmc/issue_roofline.sh
+[[ $STEPS == *,pmc* ]] && run pmc 900 bash tools/pmc/issue_roofline.sh
+[[ $STEPS == *lrnpmc* ]] && run lrnpmc 300 bash tools/pmc/learner_pmc.sh
 echo "=== done"
