@@ -1,4 +1,4 @@
 set -u
-for v in s580 d580 d600 d620 d650 s600 s620 d600; do
+for v in base nobar nosplit nol2 nodw2 nodh1 base; do
   echo "== $v"; QUADENV_LIB=tools/_build/x3_$v.so timeout -k 10 120 python tools/learner_bench.py 524288 8388608 30 2>&1 | grep quad_ppo_grad || exit 1
 done

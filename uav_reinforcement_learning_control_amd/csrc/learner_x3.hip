@@ -80,6 +80,13 @@ static_assert(2 * LB * 8 <= RND * SH * 4, "the advantage reduction aliases the r
 // swizzle: every address is affine in the k-step / tile / block indices, so each read takes one
 // base register and an immediate offset (the XOR form held ~100 hoisted address VGPRs, and spilled);
 // the 16-byte row reads are conflict-free, the 4-row transposed reads 2-way.
+// round barriers (QD_X3_NOBAR: cost-ablation builds only -- wrong results)
+#if defined(QD_X3_NOBAR)
+#define X3_BAR() ((void)0)
+#else
+#define X3_BAR() __syncthreads()
+#endif
+
 // scheduling fence between k-steps (bounds how far the compiler hoists operand reads)
 #if defined(QD_X3_NOSB)
 #define X3_SB() ((void)0)
@@ -93,6 +100,10 @@ __device__ __forceinline__ int soff(int row, int ch) { return RS * row + 16 * ch
 __device__ __forceinline__ void split2(float a, float b, bf16x2& p0, bf16x2& p1, bf16x2& p2) {
   const f32x2 x = {a, b};
   p0 = __builtin_convertvector(x, bf16x2);
+#if defined(QD_X3_NOSPLIT)  // cost-ablation builds only: one piece
+  p1 = p2 = bf16x2{};
+  return;
+#endif
   const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
   p1 = __builtin_convertvector(r1, bf16x2);
   const f32x2 r2 = r1 - __builtin_convertvector(p1, f32x2);
@@ -305,7 +316,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     bool valid[2];
 #pragma unroll
     for (int t = 0; t < 2; t++) valid[t] = base + 32 * t + l32 < s1;
-    __syncthreads();  // B1: observation image complete; the previous round's readers are done
+    X3_BAR();  // B1: observation image complete; the previous round's readers are done
 
     // ---- L1 (E form): h1^T block w of both tiles -> H1 pieces
 #pragma unroll
@@ -327,7 +338,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_H1P + p * IMG + off) = x.p[p];
       }
     }
-    __syncthreads();  // B2: H1 image complete
+    X3_BAR();  // B2: H1 image complete
 
 #if !defined(QD_X3_NOL2)
     // ---- L2 (E form): h2^T block w, A = W2 rows (registers), B = H1 row reads
@@ -381,7 +392,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         if (h == 0) Lf[B_PART / 4 + (w * RND + 32 * t + l32) * 4 + k] = part[k] + o;
       }
     }
-    __syncthreads();  // B3: head partials complete
+    X3_BAR();  // B3: head partials complete
 
     // ---- per-row loss terms and dL/d(head output) (every wave, identical arithmetic)
     float d[2][NOUT];
@@ -459,7 +470,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         *reinterpret_cast<float2*>(rowh + 8 * gg + 4 * h + 2) = make_float2(h2[t][4 * gg + 2], h2[t][4 * gg + 3]);
       }
     }
-    __syncthreads();  // B4: DH2, relu(h2) and dL/dmean images complete
+    X3_BAR();  // B4: DH2, relu(h2) and dL/dmean images complete
 
 #if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
