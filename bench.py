@@ -137,9 +137,11 @@ def _run_rank(args, rank, world, local_rank):
         g.replay()
     e1.record()
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    # the closing barrier follows this rank's clock stop: its RCCL latency (tens of us against a
+    # ~130 us 20-step region) is not step work; the MAX over ranks below is the slowest rank's K steps
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     region_us = e0.elapsed_time(e1) * 1e3 / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
