@@ -397,6 +397,12 @@ typedef struct QuadAdam {
 int64_t quad_adam_workspace_bytes(const QuadAdam* a);
 int quad_clip_adam(const QuadAdam* a, void* workspace, int64_t workspace_bytes, void* stream);
 
+/* The epoch permutation of PPO.train (SB3: np.random.permutation(buffer_size), the minibatch
+ * index source of train.py:50-68's learner): out[i], i < n, is a permutation of [0, n) keyed by
+ * `seed` -- a 4-round Feistel bijection of [0, 4^k) (4^k < 4n) restricted to [0, n) by cycle
+ * walking. Device int64 [n]; n in [1, 2^40]. */
+int quad_permutation(int64_t n, uint64_t seed, int64_t* out, void* stream);
+
 /* Device workspace (bytes) quad_ppo_grad needs for a minibatch of `batch` rows. */
 int64_t quad_ppo_workspace_bytes(int32_t batch);
 /* Which kernel quad_ppo_grad launches: 1 = k_ppo_grad_x3 (bf16 MFMA on three-piece splits of every

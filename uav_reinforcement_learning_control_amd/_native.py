@@ -98,7 +98,7 @@ EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_crea
            "quad_kernel_form", "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
            "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
            "quad_waypoints_begin", "quad_waypoints_update", "quad_ppo_workspace_bytes", "quad_ppo_grad",
-           "quad_ppo_grad_form", "quad_adam_workspace_bytes", "quad_clip_adam")
+           "quad_ppo_grad_form", "quad_permutation", "quad_adam_workspace_bytes", "quad_clip_adam")
 
 
 class QuadRollout(C.Structure):
@@ -173,6 +173,7 @@ def _declare(L):
     L.quad_ppo_workspace_bytes.restype = C.c_int64
     L.quad_ppo_grad_form.argtypes = []
     L.quad_ppo_grad_form.restype = i32
+    L.quad_permutation.argtypes = [C.c_int64, u64, vp, vp]
     L.quad_ppo_grad.argtypes = [C.POINTER(QuadPolicyParams), C.POINTER(QuadPPOBatch), C.POINTER(QuadPolicyGrads),
                                 vp, C.c_int64, vp]
     L.quad_adam_workspace_bytes.argtypes = [C.POINTER(QuadAdam)]

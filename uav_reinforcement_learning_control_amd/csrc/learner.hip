@@ -490,6 +490,40 @@ __global__ __launch_bounds__(256) void k_ppo_reduce(RArgs a) {
   }
 }
 
+// ---- the epoch permutation of PPO.train (SB3: indices = np.random.permutation(buffer_size)).
+// A keyed bijection of [0, 2^(2k)) -- a 4-round balanced Feistel network whose round function is a
+// 32-bit integer hash of (half, key, round) -- walked until it lands in [0, n) (cycle walking:
+// a permutation of the 2^(2k) >= n codes restricted to [0, n) is a permutation of [0, n); with
+// 2^(2k) < 4n the expected walk is < 4 steps). One thread per output index, no sort: the
+// torch.randperm it replaces sorts 67 M random keys per epoch (5.3 ms at config 3).
+__host__ __device__ __forceinline__ uint32_t perm_hash(uint32_t x, uint32_t k) {
+  x ^= k;
+  x *= 0x7feb352du; x ^= x >> 15;
+  x *= 0x846ca68bu; x ^= x >> 16;
+  x *= 0x7feb352du; x ^= x >> 15;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint64_t perm_feistel(uint64_t x, int half_bits, uint64_t seed) {
+  const uint32_t mask = half_bits >= 32 ? 0xffffffffu : ((1u << half_bits) - 1u);
+  uint32_t L = uint32_t(x >> half_bits) & mask, R = uint32_t(x) & mask;
+#pragma unroll
+  for (uint32_t r = 0; r < 4; r++) {
+    const uint32_t k = uint32_t(seed >> (r & 1 ? 32 : 0)) + 0x9e3779b9u * (r + 1u);
+    const uint32_t nl = R, nr = (L ^ perm_hash(R, k)) & mask;
+    L = nl; R = nr;
+  }
+  return (uint64_t(L) << half_bits) | R;
+}
+
+__global__ __launch_bounds__(256) void k_permutation(int64_t n, int half_bits, uint64_t seed, int64_t* __restrict__ out) {
+  for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
+    uint64_t x = uint64_t(i);
+    do { x = perm_feistel(x, half_bits, seed); } while (x >= uint64_t(n));
+    out[i] = int64_t(x);
+  }
+}
+
 int lfail(int code, const char* m) { return set_error(code, m); }
 
 // ---- fused clip_grad_norm_ + Adam (quad_clip_adam)
@@ -654,6 +688,17 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   r.inv_batch = 1.0f / float(b->batch); r.ent_coef = b->ent_coef;
   hipLaunchKernelGGL(k_ppo_reduce, dim3((2 * PSTRIDE + 255) / 256), dim3(256), 0, s, r);
   if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_reduce launch failed");
+  return QUAD_OK;
+}
+
+int quad_permutation(int64_t n, uint64_t seed, int64_t* out, void* stream) {
+  if (n < 1 || n > (int64_t(1) << 40) || !out) return lfail(QUAD_EINVAL, "need 1 <= n <= 2^40 and an output");
+  int bits = 2;
+  while ((int64_t(1) << bits) < n) bits += 2;  // even: a balanced Feistel on 2^bits codes, 2^bits < 4n
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(k_permutation, dim3(unsigned(blocks < 8192 ? blocks : 8192)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, bits / 2, seed, out);
+  if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_permutation launch failed");
   return QUAD_OK;
 }
 
