@@ -215,22 +215,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       wB[s][j] = W.w1[(8 * s + 64 * h + j) * H + n_own];
     }
   }
-#if defined(QD_X3_PRESPLIT_A)
-  X3 wAx[8];
-#pragma unroll
-  for (int s = 0; s < 8; s++) wAx[s] = split8(wA[s]);
-#define SPLIT_A(s) wAx[s]
-#else
+  // (the splits are loop-invariant: the compiler hoists them out of the round loop)
 #define SPLIT_A(s) split8(wA[s])
-#endif
-#if defined(QD_X3_PRESPLIT_B)
-  X3 wBx[8];
-#pragma unroll
-  for (int s = 0; s < 8; s++) wBx[s] = split8(wB[s]);
-#define SPLIT_B(s) wBx[s]
-#else
 #define SPLIT_B(s) split8(wB[s])
-#endif
   float ls[ACT], sd[ACT];
   if constexpr (NOUT == ACT) {
 #pragma unroll
@@ -239,11 +226,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 
   // accumulators (whole launch)
   f32x16 dW2[4], dW1;
-#if defined(QD_X3_DB2V)
-  float db2v[16];  // per lane (row), neuron 32w + acc_row(r, h); summed over the lanes at the end
-#pragma unroll
-  for (int r = 0; r < 16; r++) db2v[r] = 0.f;
-#endif
   f32x4 dW3[2], dM[2];  // dM[o][n] = sum_rows dL/dmean[row][o] relu'(h2[row][n]): db2 = sum_o W3[o][n] dM[o][n]
 #pragma unroll
   for (int r = 0; r < 16; r++) {
@@ -458,9 +440,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
           for (int k = 0; k < NOUT; k++) gsum = fmaf(wk[k], d[t][k], gsum);
           v[u] = h2[t][r] > 0.f ? gsum : 0.f;
-#if defined(QD_X3_DB2V)
-          db2v[r] += v[u];
-#endif
         }
         const X3h x = split4(v);
         const int off = soff(32 * t + l32, 4 * w + gg) + 8 * h;
@@ -510,9 +489,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       for (int b = 0; b < 2; b++) {
         const float hv = Lf[B_H2 / 4 + e * SH + 32 * w + 16 * b + k];
         dW3[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, hv, dW3[b], 0, 0, 0);
-#if !defined(QD_X3_DB2V)
         dM[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, hv > 0.f ? 1.f : 0.f, dM[b], 0, 0, 0);
-#endif
       }
     }
 #if !defined(QD_X3_NODH1)
@@ -597,20 +574,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         P[P_W3 + r * H + n] = dW3[b][r];
         db2 = fmaf(wk[r], dM[b][r], db2);
       }
-#if !defined(QD_X3_DB2V)
       P[P_B2 + n] = db2;
-#endif
     }
   }
-#if defined(QD_X3_DB2V)
-#pragma unroll
-  for (int r = 0; r < 16; r++) {  // db2: sum over the 32 rows (lanes) of each half, fixed order
-    float x = db2v[r];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o);
-    if (l32 == 0) P[P_B2 + 32 * w + acc_row(r, h)] = x;
-  }
-#endif
   if (w == 0) {  // lanes 0..31 hold the per-row sums (lanes 32..63 hold zeros)
     float v[NOUT + ACT + 3];
     int nv = 0;
