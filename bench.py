@@ -286,9 +286,9 @@ def _learner_kernel(m) -> dict:
     out = {"kernel": "quad_ppo_grad (k_adv_stats + %s + k_ppo_reduce)" % ("k_ppo_grad_x3" if form else "k_ppo_grad"),
            "rows": m.batch, "us_per_minibatch": us, "issued_flop": flop}
     if form:
-        # bf16x3: per 64-row round and wave 324 v_mfma_f32_32x32x16_bf16 (32 cycles each: L1 12, L2 96,
-        # dW2 96, dh1 96, dW1 24) + 64 f32 16x16x4 (dW3 and the db2 mask sums, 32 cycles each)
-        cyc = 2 * (m.batch / 64) * 4 * (324 * 32 + 64 * 32) / 1024  # per SIMD, both nets
+        # bf16x3: per 64-row round and wave 336 v_mfma_f32_32x32x16_bf16 (32 cycles each: L1 12, L2 96,
+        # dW2 96 + db2 12, dh1 96, dW1 24) + 32 f32 16x16x4 (dW3, 32 cycles each)
+        cyc = 2 * (m.batch / 64) * 4 * (336 * 32 + 32 * 32) / 1024  # per SIMD, both nets
         floor_us = cyc / 2.4e3  # at the 2.4 GHz peak clock
         out.update({"f32_equivalent_TFLOPs": flop / us / 1e6, "peak_TFLOPs": 157.3,
                     "f32_equivalent_frac": flop / us / 1e6 / 157.3,

@@ -16,8 +16,9 @@
 //   L1   h1^T = W1 x^T        E form (neurons in registers, rows on lanes)  -> H1 pieces image
 //   L2   h2^T = W2 h1^T       E form: A = W2 rows (registers), B = H1 row reads (ds_read_b128)
 //   head / loss / dL/dmean    VALU, as learner.hip
-//   dh2  E form               -> DH2 pieces image, relu(h2) -> f32 image (dW3), db2 per lane
-//   dW2  = dh2^T h1 (K = rows)  A = DH2, B = H1, both by transposed reads (ds_read_b64_tr_b16)
+//   dh2  E form               -> DH2 pieces image, relu(h2) -> f32 image (dW3)
+//   dW2  = dh2^T h1 (K = rows)  A = DH2, B = H1, both by transposed reads (ds_read_b64_tr_b16);
+//        db2 = dh2^T . ones from the same A fragments
 //   dW3  = dmean^T h2         f32 16x16x4 MFMA (small)
 //   dh1  R form (rows in registers): A = DH2 row reads, B = W2 columns (registers); relu'(h1)
 //        from the H1 image by transposed reads
@@ -226,7 +227,8 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 
   // accumulators (whole launch)
   f32x16 dW2[4], dW1;
-  f32x4 dW3[2], dM[2];  // dM[o][n] = sum_rows dL/dmean[row][o] relu'(h2[row][n]): db2 = sum_o W3[o][n] dM[o][n]
+  f32x4 dW3[2];
+  f32x16 dB2;  // db2 of neuron 32w + acc_row(r, h) in register r (every column the same): dh2^T . ones
 #pragma unroll
   for (int r = 0; r < 16; r++) {
     dW1[r] = 0.f;
@@ -234,7 +236,12 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     for (int j = 0; j < 4; j++) dW2[j][r] = 0.f;
   }
 #pragma unroll
-  for (int r = 0; r < 4; r++) { dW3[0][r] = 0.f; dW3[1][r] = 0.f; dM[0][r] = 0.f; dM[1][r] = 0.f; }
+  for (int r = 0; r < 4; r++) { dW3[0][r] = 0.f; dW3[1][r] = 0.f; }
+#pragma unroll
+  for (int r = 0; r < 16; r++) dB2[r] = 0.f;
+  bf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; j++) ones[j] = __bf16(1.f);
   float db3[NOUT], dls[ACT], st[3] = {0.f, 0.f, 0.f};  // st: pg sum, vf sum, clipped count
 #pragma unroll
   for (int k = 0; k < NOUT; k++) db3[k] = 0.f;
@@ -473,6 +480,11 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
           if (jb < 3) bn = trblk(B_H1P, s, 4 * (jb + 1) + tr_col);
           else if (s < 3) { an = trblk(B_DH2P, s + 1, 4 * w + tr_col); bn = trblk(B_H1P, s + 1, tr_col); }
           dW2[jb] = mma3(a, b, dW2[jb]);
+          if (jb == 0) {  // db2 = sum over the rows of dh2: the three pieces of dW2's A operand times ones
+            dB2 = mfma16(a.p[2], ones, dB2);
+            dB2 = mfma16(a.p[1], ones, dB2);
+            dB2 = mfma16(a.p[0], ones, dB2);
+          }
           X3_SB();
           if (jb < 3) b = bn;
           else if (s < 3) { a = an; b = bn; }
@@ -489,7 +501,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       for (int b = 0; b < 2; b++) {
         const float hv = Lf[B_H2 / 4 + e * SH + 32 * w + 16 * b + k];
         dW3[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, hv, dW3[b], 0, 0, 0);
-        dM[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, hv > 0.f ? 1.f : 0.f, dM[b], 0, 0, 0);
       }
     }
 #if !defined(QD_X3_NODH1)
@@ -564,18 +575,13 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   }
   if (lane < 16) {  // rows o < 4 of the 16x16 outputs: lanes 0..15, register o
 #pragma unroll
-    for (int b = 0; b < 2; b++) {
-      const int n = 32 * w + 16 * b + lane;
-      const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * n);
-      const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
-      float db2 = 0.f;
+    for (int b = 0; b < 2; b++)
 #pragma unroll
-      for (int r = 0; r < NOUT; r++) {
-        P[P_W3 + r * H + n] = dW3[b][r];
-        db2 = fmaf(wk[r], dM[b][r], db2);
-      }
-      P[P_B2 + n] = db2;
-    }
+      for (int r = 0; r < NOUT; r++) P[P_W3 + r * H + 32 * w + 16 * b + lane] = dW3[b][r];
+  }
+  if (l32 == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) P[P_B2 + 32 * w + acc_row(r, h)] = dB2[r];
   }
   if (w == 0) {  // lanes 0..31 hold the per-row sums (lanes 32..63 hold zeros)
     float v[NOUT + ACT + 3];
