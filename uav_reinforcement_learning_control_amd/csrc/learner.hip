@@ -201,7 +201,7 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
       float* row = L + L_H1 + (32 * t + l32) * SH + 32 * w;
 #pragma unroll
       for (int r = 0; r < 16; r += 2)  // rows acc_row(r), acc_row(r)+1 are adjacent neurons
-        *reinterpret_cast<float2*>(row + acc_row(r, h)) = make_float2(fmaxf(acc[r], 0.f), fmaxf(acc[r + 1], 0.f));
+        *reinterpret_cast<float2*>(row + acc_row(r, h)) = make_float2(relu(acc[r]), relu(acc[r + 1]));
     }
     __syncthreads();  // B2: H1 image complete
 
@@ -229,7 +229,7 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
       for (int k = 0; k < NOUT; k++) part[t][k] = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        h2[t][r] = fmaxf(h2[t][r], 0.f);
+        h2[t][r] = relu(h2[t][r]);
         const float4 w3 = *reinterpret_cast<const float4*>(L + L_W3T + 4 * (32 * w + acc_row(r, h)));
         const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
 #pragma unroll

@@ -319,8 +319,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       acc = mma3(w1x, xb, acc);
 #pragma unroll
       for (int gg = 0; gg < 4; gg++) {  // registers 4gg.. = neurons 32w + 8gg + 4h + 0..3
-        const float v[4] = {fmaxf(acc[4 * gg], 0.f), fmaxf(acc[4 * gg + 1], 0.f), fmaxf(acc[4 * gg + 2], 0.f),
-                            fmaxf(acc[4 * gg + 3], 0.f)};
+        const float v[4] = {relu(acc[4 * gg]), relu(acc[4 * gg + 1]), relu(acc[4 * gg + 2]), relu(acc[4 * gg + 3])};
         const X3h x = split4(v);
         const int off = soff(32 * t + l32, 4 * w + gg) + 8 * h;
 #pragma unroll
@@ -369,7 +368,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       for (int k = 0; k < NOUT; k++) part[k] = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        h2[t][r] = fmaxf(h2[t][r], 0.f);
+        h2[t][r] = relu(h2[t][r]);
         const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * (32 * w + acc_row(r, h)));
         const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
 #pragma unroll

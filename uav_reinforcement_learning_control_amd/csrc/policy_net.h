@@ -33,6 +33,14 @@ static_assert(ACTOR_F % 4 == 0 && LDS_F % 4 == 0, "float4 staging");
 
 __host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// ReLU as one integer max on the bits: a float with the sign bit set is a negative int32 (-0 -> +0,
+// negatives -> +0), a non-negative float keeps its bits. A float max with 0 compiles to two
+// v_max_f32 on gfx950 (first a canonicalizing max of x with itself: accumulator values are not known
+// to be canonical); the results are the same for every non-NaN x.
+__device__ __forceinline__ float relu(float x) {
+  return __builtin_bit_cast(float, max(__builtin_bit_cast(int, x), 0));
+}
+
 __device__ __forceinline__ float4 ld4(const float* L, int off) {
   return *reinterpret_cast<const float4*>(L + off);
 }
@@ -54,7 +62,7 @@ __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32
     const float4 w = ld4(L, NET_W3 + ((m * 16 + i) * 2 + h) * 4);
 #pragma unroll
     for (int j = 0; j < NT; j++) {
-      const float v = fmaxf(x[j][i], 0.f);
+      const float v = relu(x[j][i]);
       part[j][0] = fmaf(w.x, v, part[j][0]);
       part[j][1] = fmaf(w.y, v, part[j][1]);
       part[j][2] = fmaf(w.z, v, part[j][2]);
@@ -65,10 +73,10 @@ __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32
     const float4 w = ld4(L, NET_W3 + ((m * 4 + i / 4) * 2 + h) * 4);
 #pragma unroll
     for (int j = 0; j < NT; j++) {
-      part[j][0] = fmaf(w.x, fmaxf(x[j][i + 0], 0.f), part[j][0]);
-      part[j][0] = fmaf(w.y, fmaxf(x[j][i + 1], 0.f), part[j][0]);
-      part[j][0] = fmaf(w.z, fmaxf(x[j][i + 2], 0.f), part[j][0]);
-      part[j][0] = fmaf(w.w, fmaxf(x[j][i + 3], 0.f), part[j][0]);
+      part[j][0] = fmaf(w.x, relu(x[j][i + 0]), part[j][0]);
+      part[j][0] = fmaf(w.y, relu(x[j][i + 1]), part[j][0]);
+      part[j][0] = fmaf(w.z, relu(x[j][i + 2]), part[j][0]);
+      part[j][0] = fmaf(w.w, relu(x[j][i + 3]), part[j][0]);
     }
   }
 }
@@ -98,7 +106,7 @@ __device__ __forceinline__ void net_forward(const float* __restrict__ L, const f
 #pragma unroll
     for (int j = 0; j < NT; j++) {
 #pragma unroll
-      for (int r = 0; r < 16; r++) acc[j][r] = fmaxf(acc[j][r], 0.f);  // ReLU
+      for (int r = 0; r < 16; r++) acc[j][r] = relu(acc[j][r]);
       h1[j][n] = acc[j];
     }
   }
