@@ -618,6 +618,14 @@ __global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3(GArgs g) {
   else body<1>(g, lds_x3, blockIdx.x - g.nb);
 }
 
+// one net per kernel (QUADENV_LEARNER_SPLIT=1): each gets its own register allocation; the two
+// launch on two streams (fork / join by events) so their blocks share the chip
+template <int NOUT>
+__global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3_net(GArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds_x3n[];
+  body<NOUT>(g, lds_x3n, blockIdx.x);
+}
+
 }  // namespace
 
 #ifndef QD_LRN_X3_ACTOR_SHARE
@@ -634,6 +642,34 @@ int launch_ppo_grad_x3(const GArgs& g, hipStream_t s) {
                             B_TOTAL) != hipSuccess)
       return set_error(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     opted[dev] = true;
+  }
+  const char* sp = std::getenv("QUADENV_LEARNER_SPLIT");
+  if (sp && std::atoi(sp) != 0) {
+    static hipStream_t s2[64] = {};
+    static hipEvent_t ev[64][2] = {};
+    static bool ready[64] = {};
+    if (!ready[dev]) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_x3_net<ACT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, B_TOTAL) != hipSuccess ||
+          hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_x3_net<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, B_TOTAL) != hipSuccess ||
+          hipStreamCreateWithFlags(&s2[dev], hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&ev[dev][0], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&ev[dev][1], hipEventDisableTiming) != hipSuccess)
+        return set_error(QUAD_EHIP, "learner split: stream / event setup failed");
+      ready[dev] = true;
+    }
+    if (hipEventRecord(ev[dev][0], s) != hipSuccess || hipStreamWaitEvent(s2[dev], ev[dev][0], 0) != hipSuccess)
+      return set_error(QUAD_EHIP, "learner split: fork failed");
+    hipLaunchKernelGGL(k_ppo_grad_x3_net<ACT>, dim3(g.nb), dim3(LB), B_TOTAL, s, g);
+    GArgs gc = g;  // the critic kernel numbers its blocks from 0; its partials follow the actor's
+    gc.part = g.part + size_t(g.nb) * PSTRIDE;
+    gc.nb = 0;
+    hipLaunchKernelGGL(k_ppo_grad_x3_net<1>, dim3(g.nbc), dim3(LB), B_TOTAL, s2[dev], gc);
+    if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3_net launch failed");
+    if (hipEventRecord(ev[dev][1], s2[dev]) != hipSuccess || hipStreamWaitEvent(s, ev[dev][1], 0) != hipSuccess)
+      return set_error(QUAD_EHIP, "learner split: join failed");
+    return QUAD_OK;
   }
   hipLaunchKernelGGL(k_ppo_grad_x3, dim3(g.nb + g.nbc), dim3(LB), B_TOTAL, s, g);
   if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3 launch failed");
