@@ -286,3 +286,26 @@ def test_fused_update_two_ranks_stay_in_sync():
             resets = int(full[1:].sum())
     assert resets > 0  # the window covers auto-resets
     env.close()
+
+
+def test_split_kernels_match_combined(monkeypatch):
+    """QUADENV_LEARNER_SPLIT=1 (one kernel per net, two streams) computes the same bits as the
+    combined k_ppo_grad_x3 launch: same block slices, same arithmetic."""
+    from uav_reinforcement_learning_control_amd.ppo.learner import FusedLearner, _ordered
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig
+    monkeypatch.delenv("QUADENV_LEARNER", raising=False)
+    cfg = PPOConfig()
+    pol = _policy(11)
+    obs, act, logp_old, adv, ret = _buffers(pol, 40000, 11, cfg.clip_range)
+    idx = _index(pol, obs, 40000, 32768, 12)
+    out = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("QUADENV_LEARNER_SPLIT", split)
+        fl = FusedLearner(pol, cfg.clip_range, cfg.ent_coef, cfg.vf_coef, True)
+        stats = torch.zeros(4, device="cuda")
+        fl.grads(obs, act, logp_old, adv, ret, idx, stats)
+        torch.cuda.synchronize()
+        out.append(([p.grad.clone() for p in _ordered(pol)], stats.clone()))
+    for a, b in zip(out[0][0], out[1][0]):
+        assert torch.equal(a, b)
+    assert torch.equal(out[0][1], out[1][1])
