@@ -94,6 +94,7 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
     adv_mu = float(s / n);
     adv_den = float(sqrt(var)) + 1e-8f;
   }
+  const float adv_rden = 1.f / adv_den;
 
   // ---- stage the small weights in LDS, the wave's W1 / W2 fragments in registers
   for (int i = tid; i < H; i += LB) {
@@ -114,10 +115,10 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
     w2r[s] = W.w1[n_own * H + kperm(s, h)];
     w2c[s] = W.w1[kperm(s, h) * H + n_own];
   }
-  float ls[ACT], sd[ACT];
+  float ls[ACT], sd[ACT], isd[ACT];  // isd: the row loop multiplies (a full-precision division is ~10 VALU)
   if constexpr (NOUT == ACT) {
 #pragma unroll
-    for (int k = 0; k < ACT; k++) { ls[k] = g.log_std[k]; sd[k] = expf(ls[k]); }
+    for (int k = 0; k < ACT; k++) { ls[k] = g.log_std[k]; sd[k] = expf(ls[k]); isd[k] = 1.f / sd[k]; }
   }
 
   // accumulators (whole launch)
@@ -259,18 +260,18 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
         float z[ACT], lp = 0.f;
 #pragma unroll
         for (int k = 0; k < ACT; k++) {
-          z[k] = (a4k[k] - out[k]) / sd[k];
+          z[k] = (a4k[k] - out[k]) * isd[k];
           lp += -0.5f * z[k] * z[k] - ls[k] - 0.91893853320467274f;
         }
         const float r = expf(lp - SCI[e * 8 + 4]);
-        const float A = g.adv_part ? (SCI[e * 8 + 5] - adv_mu) / adv_den : SCI[e * 8 + 5];
+        const float A = g.adv_part ? (SCI[e * 8 + 5] - adv_mu) * adv_rden : SCI[e * 8 + 5];
         const float cr = fminf(fmaxf(r, 1.f - g.clip), 1.f + g.clip);
         const float sa = A * r, sb = A * cr;
         const float w1 = sa < sb ? 1.f : (sa == sb ? 0.5f : 0.f);
         const float inr = (r >= 1.f - g.clip && r <= 1.f + g.clip) ? 1.f : 0.f;
         const float dlp = valid[t] ? -g.inv_batch * A * (w1 + (1.f - w1) * inr) * r : 0.f;
 #pragma unroll
-        for (int k = 0; k < ACT; k++) d[t][k] = dlp * z[k] / sd[k];
+        for (int k = 0; k < ACT; k++) d[t][k] = dlp * z[k] * isd[k];
         if (acc_lane && valid[t]) {
           st[0] += -fminf(sa, sb);
           st[2] += fabsf(r - 1.f) > g.clip ? 1.f : 0.f;
