@@ -263,7 +263,8 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
           z[k] = (a4k[k] - out[k]) * isd[k];
           lp += -0.5f * z[k] * z[k] - ls[k] - 0.91893853320467274f;
         }
-        const float r = expf(lp - SCI[e * 8 + 4]);
+        // ratio = exp(logp - old) on the hardware exp2 (~1 ulp; the correctly rounded expf is ~10 VALU)
+        const float r = __builtin_amdgcn_exp2f((lp - SCI[e * 8 + 4]) * 1.44269504088896341f);
         const float A = g.adv_part ? (SCI[e * 8 + 5] - adv_mu) * adv_rden : SCI[e * 8 + 5];
         const float cr = fminf(fmaxf(r, 1.f - g.clip), 1.f + g.clip);
         const float sa = A * r, sb = A * cr;
