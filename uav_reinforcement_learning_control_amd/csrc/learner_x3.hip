@@ -80,7 +80,8 @@ static_assert(2 * LB * 8 <= RND * SH * 4, "the advantage reduction aliases the r
 // byte offset of 16-byte chunk `ch` of image row `row`. Padded rows (68 dwords) instead of an XOR
 // swizzle: every address is affine in the k-step / tile / block indices, so each read takes one
 // base register and an immediate offset (the XOR form held ~100 hoisted address VGPRs, and spilled);
-// the 16-byte row reads are conflict-free, the 4-row transposed reads 2-way.
+// the 16-byte row reads are conflict-free, and so are dW2's transposed reads (rows 4 apart, see
+// trblk); the relu'(h1) reads (4 consecutive rows: the accumulator's row order) are 4-way.
 // round barriers (QD_X3_NOBAR: cost-ablation builds only -- wrong results)
 #if defined(QD_X3_NOBAR)
 #define X3_BAR() ((void)0)
@@ -93,6 +94,24 @@ static_assert(2 * LB * 8 <= RND * SH * 4, "the advantage reduction aliases the r
 #define X3_SB() ((void)0)
 #else
 #define X3_SB() __builtin_amdgcn_sched_barrier(0)
+#endif
+
+// The next k-step's operand reads interleaved with the first MFMAs of this one (scheduling groups
+// of the region between two X3_SB fences: `n_rd` LDS reads, `n_mfma` MFMAs). Left to itself the
+// scheduler sinks the reads behind all but the last MFMA (their registers are the ones the current
+// MFMAs read), so each k-step waited out the LDS latency: 1.5 % of the kernel (QD_X3_NOPIPE:
+// A/B builds only)
+#if !defined(QD_X3_NOPIPE)
+#define X3_PIPE(n_rd, n_mfma)                                                   \
+  do {                                                                          \
+    for (int i_ = 0; i_ < (n_rd) / 2; i_++) {                                   \
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                        \
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);                        \
+    }                                                                           \
+    __builtin_amdgcn_sched_group_barrier(0x008, (n_mfma) - (n_rd) / 2, 0);      \
+  } while (0)
+#else
+#define X3_PIPE(n_rd, n_mfma) ((void)0)
 #endif
 
 __device__ __forceinline__ int soff(int row, int ch) { return RS * row + 16 * ch; }
@@ -353,6 +372,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         }
 #pragma unroll
         for (int t = 0; t < 2; t++) h2[t] = mma3(a, b[t], h2[t]);
+        if (s < 7) X3_PIPE(6, 12);
         X3_SB();
         if (s < 7) { a = an; b[0] = bn[0]; b[1] = bn[1]; }
       }
@@ -462,13 +482,17 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
     {  // 20 operand blocks (per k-step s: A, then B of jb = 0..3), each read one unit ahead
+      // The K order over the rows is free (both operands use it): the 4-row blocks of the transposed
+      // reads take rows 4 apart (k-step s, lane half h: element j is row 16s + 2h + (j >> 2) + 4(j & 3)),
+      // so a block's rows sit 16 banks apart on the 272-byte rows and a 32-lane half covers the 64
+      // banks once (consecutive rows were 4-way conflicts)
       auto trblk = [&](int img, int s, int chunk) {
-        const int r0 = 16 * s + 8 * h + gq;
+        const int r0 = 16 * s + 2 * h + 4 * gq;
         X3 x;
 #pragma unroll
         for (int p = 0; p < 3; p++) {
           const char* I = L + img + p * IMG;
-          x.p[p] = cat_tr(rdtr(I, soff(r0, chunk) + tr_half), rdtr(I, soff(r0 + 4, chunk) + tr_half));
+          x.p[p] = cat_tr(rdtr(I, soff(r0, chunk) + tr_half), rdtr(I, soff(r0 + 1, chunk) + tr_half));
         }
         return x;
       };
@@ -486,6 +510,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
             dB2 = mfma16(a.p[1], ones, dB2);
             dB2 = mfma16(a.p[0], ones, dB2);
           }
+          if (jb == 0) X3_PIPE(6, 9);
+          else if (jb < 3) X3_PIPE(6, 6);
+          else if (s < 3) X3_PIPE(12, 6);
           X3_SB();
           if (jb < 3) b = bn;
           else if (s < 3) { a = an; b = bn; }
@@ -527,6 +554,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         }
 #pragma unroll
         for (int t = 0; t < 2; t++) dh1[t] = mma3(a[t], b, dh1[t]);
+        if (s < 7) X3_PIPE(6, 12);
         X3_SB();
         if (s < 7) { b = bn; a[0] = an[0]; a[1] = an[1]; }
       }
