@@ -116,28 +116,33 @@ def _run_rank(args, rank, world, local_rank):
     step = _quad_step_fn(env)
     chunk = args.graph_chunk if args.steps % args.graph_chunk == 0 else args.steps
 
+    def region(graphs):
+        """barrier + synchronize, the replays between two HIP events (on the stream the kernels
+        run on: the device time of the same region), synchronize; returns (wall s, e0, e1)"""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()
+        for gr in graphs:
+            gr.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, e0, e1
+
     # the timed step sequence as hipGraph(s), captured and uploaded before the warmup; the W
-    # warmup steps are replays of a graph of the same launches (first kernel runs, caches, TLB)
+    # warmup steps are replays of a graph of the same launches (first kernel runs, caches, TLB),
+    # run through the timed region's own host path: its first execution in a process costs ~10 us
+    # of host time (event records, synchronize; profiles/r02/first_region.txt), setup, not steps
     g = _graph_of(step, actions, args.warmup, chunk)
     if args.warmup > 0:
         gw = _graph_of(step, actions, 0, args.warmup)
-        gw.replay()
-    torch.cuda.synchronize()
+        region([gw])
 
-    # timed region: exactly K steps, barrier + synchronize on both sides; HIP events on the stream
-    # the kernels run on give the device time per step inside the same region
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record()
-    for _ in range(args.steps // chunk):
-        g.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    # timed region: exactly K steps, barrier + synchronize on both sides
+    elapsed, e0, e1 = region([g] * (args.steps // chunk))
     # the closing barrier follows this rank's clock stop: its RCCL latency (tens of us against a
     # ~130 us 20-step region) is not step work; the MAX over ranks below is the slowest rank's K steps
     if world > 1:

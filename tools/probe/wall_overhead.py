@@ -44,6 +44,26 @@ def main():
     else:
         g.replay()
     torch.cuda.synchronize()
+    if os.environ.get("WARM_G") == "1":  # replay the timed graph once more before the first trial
+        g.replay()
+        torch.cuda.synchronize()
+    spin = int(os.environ.get("SPIN_CYCLES", "0"))  # a spin kernel (no step) right before trial 0
+    if spin:
+        torch.cuda._sleep(spin)
+        torch.cuda.synchronize()
+    if os.environ.get("DRY") == "1":  # the timed region's host path once with no launches in it
+        torch.cuda.synchronize()
+        d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        d0.record()
+        d1.record()
+        torch.cuda.synchronize()
+    if os.environ.get("DRYG") == "1":  # ... and with the warm-up graph's steps (bench: warm-up then region)
+        torch.cuda.synchronize()
+        d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        d0.record()
+        gw.replay()
+        d1.record()
+        torch.cuda.synchronize()
     sub, wait, wall, dev_us = [], [], [], []
     for _ in range(trials):
         torch.cuda.synchronize()
@@ -64,7 +84,8 @@ def main():
         wall.append((t2 - t0) * 1e6 / k)
         dev_us.append(e0.elapsed_time(e1) * 1e3 / k)
     med = statistics.median
-    print("first trials wall/step:", " ".join(f"{w:.2f}" for w in wall[:4]))
+    print("first trials wall/step:", " ".join(f"{w:.2f}" for w in wall[:4]),
+          "| device/step:", " ".join(f"{d:.2f}" for d in dev_us[:4]))
     print(f"{mode:6s} chunk={chunk} n={n} K={k}: wall/step median {med(wall):.2f} us (min {min(wall):.2f}, max {max(wall):.2f}); "
           f"device/step {med(dev_us):.2f}; submit {med(sub):.1f} us, sync wait {med(wait):.1f} us per region")
 
