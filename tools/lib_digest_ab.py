@@ -40,8 +40,23 @@ def child():
     t = [min(run(0, n, steps=1000) for _ in range(3)) for n in (4096, 65536)]
     d = [digest("hover", None, "basic"), digest("hover", "RateControlWrapper", "full"),
          digest("trajectory", None, "full"), digest("trajectory", "RateControlWrapper", "basic")]
+    import torch
+    import bench
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    dev = torch.device("cuda", 0)
+    kr = [bench._kstep_rate(n, k, dev, 0)["us_per_step"] for n, k in ((4096, 1000), (65536, 200))]
+    e = QuadVecEnv(4096, env="hover", device=dev, seed=5)
+    e.reset()
+    r = e.step_random(300, actions=True)
+    h = hashlib.sha256()
+    for k in sorted(r):
+        h.update(r[k].cpu().numpy().tobytes())
+    for v in e.get_state().values():
+        h.update(v.tobytes())
+    e.close()
     print(f"{os.path.basename(os.environ.get('QUADENV_LIB', 'base')):18s} 4096: {t[0]:.3f} us  "
-          f"65536: {t[1]:.3f} us  digests {' '.join(d)}", flush=True)
+          f"65536: {t[1]:.3f} us  K-step 4096: {kr[0]:.3f}  65536: {kr[1]:.3f} us/step  "
+          f"digests {' '.join(d)} {h.hexdigest()[:16]}", flush=True)
 
 
 def main():

@@ -273,26 +273,32 @@ __device__ __forceinline__ void step_body(const KConsts<float>& K, KParams p, co
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_step_h<KIND, CTBR, SPEC>: the step with HELPER waves. A 512-thread block owns 256 envs: waves
-// 0-3 step one env per lane exactly as k_step; waves 4-7 -- one beside each step wave on its SIMD --
+// k_step_h<KIND, CTBR, SPEC>: the step with HELPER waves. A block of 2 x HB threads owns HB envs:
+// the first HB/64 waves step one env per lane exactly as k_step; as many helper waves --
 // meanwhile draw every env's NEXT reset (the Philox words of its episode counter, the affine map,
 // the quaternion, the reset observation: reset_block / reset_affine_u / env_reset_from, the same
 // functions, so the same bits) into an LDS image, and after the block barrier a resetting step lane
 // only copies its row. The draw had been on the lone step wave's path (0.72 us of a 6.5 us step at
 // 65,536 envs, ablation build); the helpers run it in the issue slots the stalled step wave leaves.
+// HB = envs per block (one step wave + its helper wave per 64). Small batches take 64: at 4,096
+// envs 3.79 vs 4.24 us per launch with 256 (the batch spreads over 64 CUs instead of 16, and each
+// barrier joins two waves instead of eight); at 65,536 the two measured equal (5.84-5.87 vs
+// 5.83-5.87 us) and 128 slower (6.10), so batches above H_SMALL keep 256
+// (profiles/r02/ab_step_h_block.txt).
+constexpr int H_SMALL = 32768;
 constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
-template <int KIND, bool CTBR>
+template <int KIND, bool CTBR, int HB>
 __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, const float4* __restrict__ act,
                                             QuadStepOut out, float4* lds, float* H) {
   const int tid = threadIdx.x;
-  const int block_first = p.first + blockIdx.x * BLOCK;
+  const int block_first = p.first + blockIdx.x * HB;
   const int end = p.first + p.count;
-  const int l = tid & (BLOCK - 1);
+  const int l = tid & (HB - 1);
   const bool live = block_first + l < end;
   const int i = live ? block_first + l : end - 1;
   const Tiles S(p);
   const uint32_t vo = env_off(uint32_t(i));
-  if (tid >= BLOCK) {  // ---- helper: env i's next reset, into H[f][l]
+  if (tid >= HB) {  // ---- helper: env i's next reset, into H[f][l]
     const uint32_t ep = S.ldu(F_EP, vo);
     float u16[16];
 #pragma unroll
@@ -312,7 +318,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
                              obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9],
                              obs[10], obs[11]};
 #pragma unroll
-    for (int f = 0; f < HROW; f++) H[f * BLOCK + l] = row[f];
+    for (int f = 0; f < HROW; f++) H[f * HB + l] = row[f];
     __syncthreads();  // (1) the image is complete
     __syncthreads();  // (2) the obs rows are staged
   } else {  // ---- step
@@ -349,7 +355,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
       if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
       float row[HROW];
 #pragma unroll
-      for (int f = 0; f < HROW; f++) row[f] = H[f * BLOCK + l];
+      for (int f = 0; f < HROW; f++) row[f] = H[f * HB + l];
 #pragma unroll
       for (int j = 0; j < 3; j++) {
         e.pos[j] = row[j]; e.v[j] = row[7 + j]; e.w[j] = row[10 + j]; e.target[j] = row[13 + j];
@@ -369,25 +375,25 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
     __syncthreads();  // (2)
   }
-  // the block's [256,12] obs rows as contiguous float4 stores, shared by all 512 threads
-  const int nf4 = min(BLOCK, end - block_first) * 3;
+  // the block's [HB,12] obs rows as contiguous float4 stores, shared by all 2 x HB threads
+  const int nf4 = min(HB, end - block_first) * 3;
   float4* dst = reinterpret_cast<float4*>(out.obs + size_t(block_first) * 12);
-  for (int idx = tid; idx < nf4; idx += 2 * BLOCK) dst[idx] = lds[idx];
+  for (int idx = tid; idx < nf4; idx += 2 * HB) dst[idx] = lds[idx];
 }
 
-template <int KIND, bool CTBR, bool SPEC>
-__global__ __launch_bounds__(2 * BLOCK) void k_step_h(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
+template <int KIND, bool CTBR, bool SPEC, int HB>
+__global__ __launch_bounds__(2 * HB) void k_step_h(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
                                                       int32_t first, int32_t count,
                                                       const KConsts<float>* __restrict__ kc, KParams p, QuadStepOut out) {
   p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
   p.kc = kc;
-  __shared__ float4 lds[BLOCK * 3];
-  __shared__ float H[HROW * BLOCK];
+  __shared__ float4 lds[HB * 3];
+  __shared__ float H[HROW * HB];
   if constexpr (SPEC) {
     constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
-    step_h_body<KIND, CTBR>(K, p, act, out, lds, H);
+    step_h_body<KIND, CTBR, HB>(K, p, act, out, lds, H);
   } else {
-    step_h_body<KIND, CTBR>(*kc, p, act, out, lds, H);
+    step_h_body<KIND, CTBR, HB>(*kc, p, act, out, lds, H);
   }
 }
 
@@ -471,6 +477,12 @@ __device__ __forceinline__ void step_random_body(const KConsts<float>& K, KParam
   }
 }
 
+// Envs per k_step_random_h block: 256 (64 measured faster at 4,096 envs, 2.22 vs 2.40 us per step,
+// but slower at 65,536, 4.5 vs 3.4: profiles/r02/ab_step_h_block.txt). A/B builds: QD_RB.
+#if !defined(QD_RB)
+#define QD_RB 256
+#endif
+constexpr int RB = QD_RB;
 // The same with helper waves (see k_step_h): a 512-thread block owns 256 envs; waves 0-3 step them,
 // waves 4-7 draw -- two steps ahead -- each env's actions (quad_random_actions' Philox map) into a
 // double-buffered LDS slot, and keep each env's next-reset row (k_step_h's image) current: after
@@ -498,7 +510,7 @@ __device__ __forceinline__ void helper_reset_row(const KConsts<float>& K, const 
                            obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9],
                            obs[10], obs[11]};
 #pragma unroll
-  for (int f = 0; f < HROW; f++) H[f * BLOCK + l] = row[f];
+  for (int f = 0; f < HROW; f++) H[f * RB + l] = row[f];
 }
 
 // a resetting step lane takes its row of the helper image (k_step_h, k_step_random_h)
@@ -507,7 +519,7 @@ __device__ __forceinline__ void take_reset_row(const KConsts<float>& K, const fl
                                                float obs[12]) {
   float row[HROW];
 #pragma unroll
-  for (int f = 0; f < HROW; f++) row[f] = H[f * BLOCK + l];
+  for (int f = 0; f < HROW; f++) row[f] = H[f * RB + l];
 #pragma unroll
   for (int j = 0; j < 3; j++) {
     e.pos[j] = row[j]; e.v[j] = row[7 + j]; e.w[j] = row[10 + j]; e.target[j] = row[13 + j];
@@ -533,22 +545,22 @@ __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KPar
                                                    float4* __restrict__ act_out, uint32_t step0, int32_t steps,
                                                    float4* lds, float* H, float4* A, uint32_t* R) {
   const int tid = threadIdx.x;
-  const int block_first = blockIdx.x * BLOCK;
+  const int block_first = blockIdx.x * RB;
   const int n = p.n;
-  const int l = tid & (BLOCK - 1);
+  const int l = tid & (RB - 1);
   const bool live = block_first + l < n;
   const int i = live ? block_first + l : n - 1;
   const Tiles S(p);
   const uint32_t vo = env_off(uint32_t(i));
   const uint64_t gid = p.gid_base + uint64_t(i);
-  const bool helper = tid >= BLOCK;
-  const int nf4 = min(BLOCK, n - block_first) * 3;
+  const bool helper = tid >= RB;
+  const int nf4 = min(RB, n - block_first) * 3;
   EnvRegs<float> e;
   uint32_t ep = 0;
   if (helper) {
     ep = S.ldu(F_EP, vo);
     A[l] = random_action4(p.seed, gid, step0);
-    if (steps > 1) A[BLOCK + l] = random_action4(p.seed, gid, step0 + 1u);
+    if (steps > 1) A[RB + l] = random_action4(p.seed, gid, step0 + 1u);
     helper_reset_row<KIND, CTBR>(K, p, i, ep, H, l);
   } else {
     load_env(p, i, e, CTBR);
@@ -557,7 +569,7 @@ __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KPar
   for (int t = 0; t < steps; t++) {
     const uint32_t row = uint32_t(t) * uint32_t(n) + uint32_t(i);  // time-major row (< 2^32: checked)
     if (!helper) {
-      const float4 a4 = A[(t & 1) * BLOCK + l];
+      const float4 a4 = A[(t & 1) * RB + l];
       const float a[4] = {a4.x, a4.y, a4.z, a4.w};
       StepRes r;
       env_step<float, CTBR>(K, e, a, r);
@@ -581,17 +593,17 @@ __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KPar
       lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
       __syncthreads();  // (B) obs rows and reset flags staged
     } else {
-      if (act_out && live) sto(act_out, 16u * row, A[(t & 1) * BLOCK + l]);
+      if (act_out && live) sto(act_out, 16u * row, A[(t & 1) * RB + l]);
       __syncthreads();  // (A)
       __syncthreads();  // (B)
       if (R[l]) {  // this env reset at step t: its next episode's row
         ep += 1u;
         helper_reset_row<KIND, CTBR>(K, p, i, ep, H, l);
       }
-      if (t + 2 < steps) A[(t & 1) * BLOCK + l] = random_action4(p.seed, gid, step0 + uint32_t(t + 2));
+      if (t + 2 < steps) A[(t & 1) * RB + l] = random_action4(p.seed, gid, step0 + uint32_t(t + 2));
     }
     float4* dst = reinterpret_cast<float4*>(out.obs + (size_t(t) * size_t(n) + size_t(block_first)) * 12);
-    for (int idx = tid; idx < nf4; idx += 2 * BLOCK) dst[idx] = lds[idx];
+    for (int idx = tid; idx < nf4; idx += 2 * RB) dst[idx] = lds[idx];
   }
   if (live) {
     if (helper) S.stu(F_EP, vo, ep);
@@ -600,14 +612,14 @@ __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KPar
 }
 
 template <int KIND, bool CTBR, bool SPEC>
-__global__ __launch_bounds__(2 * BLOCK) void k_step_random_h(const KConsts<float>* __restrict__ kc, KParams p,
+__global__ __launch_bounds__(2 * RB) void k_step_random_h(const KConsts<float>* __restrict__ kc, KParams p,
                                                              QuadStepOut out, float4* __restrict__ act_out,
                                                              uint32_t step0, int32_t steps) {
   p.kc = kc;
-  __shared__ float4 lds[BLOCK * 3];
-  __shared__ float H[HROW * BLOCK];
-  __shared__ float4 A[2 * BLOCK];
-  __shared__ uint32_t R[BLOCK];
+  __shared__ float4 lds[RB * 3];
+  __shared__ float H[HROW * RB];
+  __shared__ float4 A[2 * RB];
+  __shared__ uint32_t R[RB];
   if constexpr (SPEC) {
     constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
     step_random_h_body<KIND, CTBR>(K, p, out, act_out, step0, steps, lds, H, A, R);
@@ -1633,18 +1645,21 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, QD_KARGS);     \
   else                                                                                          \
     hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, QD_KARGS);
-#define QD_LAUNCH_H(SP)                                                                            \
+#define QD_LAUNCH_H(SP, HB)                                                                            \
   if (traj && ctbr)                                                                             \
-    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, true, SP>), grid, blk2, 0, s, QD_KARGS);      \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, true, SP, HB>), grid, blk2, 0, s, QD_KARGS);      \
   else if (traj)                                                                                \
-    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, false, SP>), grid, blk2, 0, s, QD_KARGS);     \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, false, SP, HB>), grid, blk2, 0, s, QD_KARGS);     \
   else if (ctbr)                                                                                \
-    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, true, SP>), grid, blk2, 0, s, QD_KARGS);     \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, true, SP, HB>), grid, blk2, 0, s, QD_KARGS);     \
   else                                                                                          \
-    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, false, SP>), grid, blk2, 0, s, QD_KARGS);
-    const dim3 blk2(2 * BLOCK);
-    if (h->helper) {
-      if (h->spec) { QD_LAUNCH_H(true) } else { QD_LAUNCH_H(false) }
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, false, SP, HB>), grid, blk2, 0, s, QD_KARGS);
+    if (h->helper && count <= H_SMALL) {
+      const dim3 grid(unsigned((int64_t(count) + 63) / 64)), blk2(128);
+      if (h->spec) { QD_LAUNCH_H(true, 64) } else { QD_LAUNCH_H(false, 64) }
+    } else if (h->helper) {
+      const dim3 grid(unsigned((int64_t(count) + 255) / 256)), blk2(512);
+      if (h->spec) { QD_LAUNCH_H(true, 256) } else { QD_LAUNCH_H(false, 256) }
     } else if (h->spec) { QD_LAUNCH_K(true) } else { QD_LAUNCH_K(false) }
 #undef QD_LAUNCH_K
 #undef QD_LAUNCH_H
@@ -1752,8 +1767,9 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
     hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, true, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
   else                                                                                                   \
     hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, false, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-  const dim3 blk2(2 * BLOCK);
+  const dim3 blk2(2 * RB);
   if (h->helper) {
+    const dim3 grid(unsigned((int64_t(h->n) + RB - 1) / RB));
     if (h->spec) { QD_LAUNCH_RH(true) } else { QD_LAUNCH_RH(false) }
   } else if (h->spec) { QD_LAUNCH_R(true) } else { QD_LAUNCH_R(false) }
 #undef QD_LAUNCH_R
