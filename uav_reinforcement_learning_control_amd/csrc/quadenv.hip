@@ -477,19 +477,15 @@ __device__ __forceinline__ void step_random_body(const KConsts<float>& K, KParam
   }
 }
 
-// Envs per k_step_random_h block: 256 (64 measured faster at 4,096 envs, 2.22 vs 2.40 us per step,
-// but slower at 65,536, 4.5 vs 3.4: profiles/r02/ab_step_h_block.txt). A/B builds: QD_RB.
-#if !defined(QD_RB)
-#define QD_RB 256
-#endif
-constexpr int RB = QD_RB;
+// RB = envs per k_step_random_h block: 64 up to H_SMALL envs (4,096 envs: 2.22 vs 2.40 us per
+// step with 256), 256 above (65,536: 3.4 vs 4.5 us with 64); profiles/r02/ab_step_h_block.txt.
 // The same with helper waves (see k_step_h): a 512-thread block owns 256 envs; waves 0-3 step them,
 // waves 4-7 draw -- two steps ahead -- each env's actions (quad_random_actions' Philox map) into a
 // double-buffered LDS slot, and keep each env's next-reset row (k_step_h's image) current: after
 // every step they read which envs reset, advance those episode counters and redraw their rows.
 // Per step: barrier A (flags known; the image is current) -> resets copied, obs rows staged ->
 // barrier B -> obs rows stored by all 512 threads, helpers redraw. Same bits as k_step_random.
-template <int KIND, bool CTBR>
+template <int KIND, bool CTBR, int RB>
 __device__ __forceinline__ void helper_reset_row(const KConsts<float>& K, const KParams& p, int i, uint32_t ep,
                                                  float* H, int l) {
   float u16[16];
@@ -514,7 +510,7 @@ __device__ __forceinline__ void helper_reset_row(const KConsts<float>& K, const 
 }
 
 // a resetting step lane takes its row of the helper image (k_step_h, k_step_random_h)
-template <int KIND>
+template <int KIND, int RB>
 __device__ __forceinline__ void take_reset_row(const KConsts<float>& K, const float* H, int l, EnvRegs<float>& e,
                                                float obs[12]) {
   float row[HROW];
@@ -540,7 +536,7 @@ __device__ __forceinline__ float4 random_action4(uint64_t seed, uint64_t gid, ui
                      float(c[2] >> 8) * 0x1p-23f - 1.0f, float(c[3] >> 8) * 0x1p-23f - 1.0f);
 }
 
-template <int KIND, bool CTBR>
+template <int KIND, bool CTBR, int RB>
 __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KParams p, QuadStepOut out,
                                                    float4* __restrict__ act_out, uint32_t step0, int32_t steps,
                                                    float4* lds, float* H, float4* A, uint32_t* R) {
@@ -561,7 +557,7 @@ __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KPar
     ep = S.ldu(F_EP, vo);
     A[l] = random_action4(p.seed, gid, step0);
     if (steps > 1) A[RB + l] = random_action4(p.seed, gid, step0 + 1u);
-    helper_reset_row<KIND, CTBR>(K, p, i, ep, H, l);
+    helper_reset_row<KIND, CTBR, RB>(K, p, i, ep, H, l);
   } else {
     load_env(p, i, e, CTBR);
   }
@@ -585,7 +581,7 @@ __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KPar
       __syncthreads();  // (A) the image holds every env's next reset
       if (rs) {
         if (out.terminal_obs) store_row12(out.terminal_obs, row, r.obs);
-        take_reset_row<KIND>(K, H, l, e, obs);
+        take_reset_row<KIND, RB>(K, H, l, e, obs);
       }
       R[l] = rs ? 1u : 0u;
       lds[3 * l + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
@@ -598,7 +594,7 @@ __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KPar
       __syncthreads();  // (B)
       if (R[l]) {  // this env reset at step t: its next episode's row
         ep += 1u;
-        helper_reset_row<KIND, CTBR>(K, p, i, ep, H, l);
+        helper_reset_row<KIND, CTBR, RB>(K, p, i, ep, H, l);
       }
       if (t + 2 < steps) A[(t & 1) * RB + l] = random_action4(p.seed, gid, step0 + uint32_t(t + 2));
     }
@@ -611,7 +607,7 @@ __device__ __forceinline__ void step_random_h_body(const KConsts<float>& K, KPar
   }
 }
 
-template <int KIND, bool CTBR, bool SPEC>
+template <int KIND, bool CTBR, bool SPEC, int RB>
 __global__ __launch_bounds__(2 * RB) void k_step_random_h(const KConsts<float>* __restrict__ kc, KParams p,
                                                              QuadStepOut out, float4* __restrict__ act_out,
                                                              uint32_t step0, int32_t steps) {
@@ -622,9 +618,9 @@ __global__ __launch_bounds__(2 * RB) void k_step_random_h(const KConsts<float>* 
   __shared__ uint32_t R[RB];
   if constexpr (SPEC) {
     constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
-    step_random_h_body<KIND, CTBR>(K, p, out, act_out, step0, steps, lds, H, A, R);
+    step_random_h_body<KIND, CTBR, RB>(K, p, out, act_out, step0, steps, lds, H, A, R);
   } else {
-    step_random_h_body<KIND, CTBR>(*kc, p, out, act_out, step0, steps, lds, H, A, R);
+    step_random_h_body<KIND, CTBR, RB>(*kc, p, out, act_out, step0, steps, lds, H, A, R);
   }
 }
 
@@ -1758,19 +1754,21 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
     hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
   else                                                                                                   \
     hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-#define QD_LAUNCH_RH(SP)                                                                                     \
+#define QD_LAUNCH_RH(SP, RB)                                                                                     \
   if (traj && ctbr)                                                                                      \
-    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_TRAJ, true, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);   \
+    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_TRAJ, true, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);   \
   else if (traj)                                                                                         \
-    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_TRAJ, false, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
+    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_TRAJ, false, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
   else if (ctbr)                                                                                         \
-    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, true, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
+    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, true, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
   else                                                                                                   \
-    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, false, SP>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-  const dim3 blk2(2 * RB);
-  if (h->helper) {
-    const dim3 grid(unsigned((int64_t(h->n) + RB - 1) / RB));
-    if (h->spec) { QD_LAUNCH_RH(true) } else { QD_LAUNCH_RH(false) }
+    hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, false, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
+  if (h->helper && h->n <= H_SMALL) {
+    const dim3 grid(unsigned((int64_t(h->n) + 63) / 64)), blk2(128);
+    if (h->spec) { QD_LAUNCH_RH(true, 64) } else { QD_LAUNCH_RH(false, 64) }
+  } else if (h->helper) {
+    const dim3 grid(unsigned((int64_t(h->n) + 255) / 256)), blk2(512);
+    if (h->spec) { QD_LAUNCH_RH(true, 256) } else { QD_LAUNCH_RH(false, 256) }
   } else if (h->spec) { QD_LAUNCH_R(true) } else { QD_LAUNCH_R(false) }
 #undef QD_LAUNCH_R
 #undef QD_LAUNCH_RH
