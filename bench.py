@@ -103,6 +103,20 @@ def _kernel_name(env) -> str:
     return name + (f" ({', '.join(tags)})" if tags else "")
 
 
+def _kernel_symbol(env) -> str:
+    """The launched hover step kernel's template symbol as rocprofv3 names it (csrc/quadenv.hip
+    quad_step_range: k_step_h<KIND, CTBR, SPEC, HB> with HB = 64 up to 32,768 envs, else 256;
+    k_step<KIND, CTBR, SPEC>; k_step_g<KIND, CTBR, G, SPEC>)."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    form = int(N.lib().quad_kernel_form(env._h))
+    lanes, spec = form & 15, "true" if form & 16 else "false"
+    if lanes:
+        return f"k_step_g<0, false, {lanes}, {spec}>"
+    if form & 32:
+        return f"k_step_h<0, false, {spec}, {64 if env.num_envs <= 32768 else 256}>"
+    return f"k_step<0, false, {spec}>"
+
+
 def _run_rank(args, rank, world, local_rank):
     from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
 
@@ -156,7 +170,7 @@ def _run_rank(args, rank, world, local_rank):
     # per-launch kernel time (roofline) on the same kernel, stream and data
     res = dict(elapsed=elapsed, region_us=region_us,
                kernel_us=_gated_kernel_us(step, actions, args.kernel_launches),
-               kernel=_kernel_name(env))
+               kernel=_kernel_name(env), symbol=_kernel_symbol(env))
     if args.rollout_steps > 0:
         res["rollout"] = _rollout_phase(env, args)
     if args.e2e_iters > 0:
@@ -179,6 +193,7 @@ def _run_rank(args, rank, world, local_rank):
         for k in range(50):  # past the post-reset transient: ~11 % of envs reset per step from here on
             st(acts[k % 8].data_ptr())
         res["large_kernel_us"] = _gated_kernel_us(st, acts, 200)
+        res["large_symbol"] = _kernel_symbol(big)
         big.close()
     else:
         env.close()
@@ -505,14 +520,21 @@ def _cpu_baseline_ppo(seconds: float, threads: int = 1) -> dict:
         torch.set_num_threads(old_threads)
 
 
-def _pmc_traffic(n_envs: int):
-    """HBM bytes per quad_step launch from the committed rocprofv3 PMC summary, if present."""
-    path = os.path.join(REPO, "profiles", "pmc_quad_step.json")
+def _pmc_traffic(symbol: str, n_envs: int):
+    """HBM-side bytes per launch of THIS kernel at this size from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json, tools/pmc/traffic_summary.py, keyed by kernel symbol and env count),
+    or None when no pass of the kernel the bench timed exists."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
-        return d.get(str(n_envs), {}).get("hbm_bytes_per_launch")
+        rec = d.get("kernels", {}).get(symbol, {}).get(str(n_envs))
+        if not rec:
+            return None
+        return {"bytes_per_launch": rec["hbm_bytes_per_launch"], "kernel": symbol, "envs": n_envs,
+                "traffic_over_algorithmic": rec["traffic_over_algorithmic"], "round": d.get("round"),
+                "source": "profiles/pmc_traffic.json"}
     except Exception:
         return None
 
@@ -634,7 +656,7 @@ def main():
     value = n_total * args.steps / res["elapsed"]
     kus = res["kernel_us"]
     achieved = BYTES_PER_ENV_STEP * args.envs / (kus * 1e-6) / 1e9
-    traffic = _pmc_traffic(args.envs)
+    traffic = _pmc_traffic(res["symbol"], args.envs)
     line = {
         "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -647,8 +669,9 @@ def main():
                    "parallelism": f"env-shard x{world} (no data-path collective)"},
         "device_us_per_step": res["region_us"],
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": res["kernel"], "kernel_us": kus,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_pmc": traffic,
+                     "kernel": res["kernel"], "kernel_symbol": res["symbol"], "kernel_us": kus,
                      "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs,
                      "issue": _pmc_issue(args.envs)},
     }
@@ -663,7 +686,9 @@ def main():
         line["large_batch"] = {"envs": args.large_envs, "kernel_us": lk,
                                "env_steps_per_s_kernel": args.large_envs / (lk * 1e-6),
                                "achieved_GBs": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9,
-                               "frac": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9 / HBM_PEAK_GBS}
+                               "frac": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                               "kernel_symbol": res["large_symbol"],
+                               "traffic_pmc": _pmc_traffic(res["large_symbol"], args.large_envs)}
     if not args.no_cpu_baseline and world == 1:
         cores = _cpu_info()["usable_cores"]
         line["cpu_host"] = _cpu_info()

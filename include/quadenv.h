@@ -42,8 +42,12 @@ enum { QUAD_OK = 0, QUAD_EINVAL = -1, QUAD_EHIP = -2, QUAD_ENOMEM = -3, QUAD_EMO
  * semantics (no MuJoCo-C bad-state resets). */
 enum { QUAD_ENV_HOVER = 0, QUAD_ENV_TRAJ = 1, QUAD_ENV_BRAX_HOVER = 2, QUAD_ENV_BRAX_TRAJ = 3 };
 /* QUAD_WRAP_RELPOS: RelPosActWrapper (envs/wrappers.py:13-25): 7-D obs [normalized rel pos (3),
- * previous action (4)] of the hover / trajectory kinds (quad_step's obs is then [N,7]). */
-enum { QUAD_WRAP_NONE = 0, QUAD_WRAP_CTBR = 1, QUAD_WRAP_RELPOS = 2 };
+ * previous action (4)] of the hover / trajectory kinds (quad_step's obs is then [N,7]).
+ * QUAD_WRAP_CTBR_RELPOS: the stack the reference README documents,
+ * RelPosActWrapper(RateControlWrapper(env)): the CTBR controller maps the rate action to torques
+ * (rate_wrapper.py:69-98) and the 7-D obs carries the RATE action as the previous action
+ * (rate_wrapper.py:100-106 overwrites unwrapped._prev_action after the base step). */
+enum { QUAD_WRAP_NONE = 0, QUAD_WRAP_CTBR = 1, QUAD_WRAP_RELPOS = 2, QUAD_WRAP_CTBR_RELPOS = 3 };
 enum { QUAD_NQ = 11, QUAD_NV = 10, QUAD_OBS = 12, QUAD_OBS_BRAX = 21, QUAD_OBS_RELPOS = 7, QUAD_ACT = 4 };
 
 /* Env configuration. quad_default_cfg() fills the reference's defaults:
@@ -52,7 +56,7 @@ enum { QUAD_NQ = 11, QUAD_NV = 10, QUAD_OBS = 12, QUAD_OBS_BRAX = 21, QUAD_OBS_R
  *  pid_gains.json:43-52, drone_config.py:9-22, drone.xml:4 (timestep, gravity, fluid). */
 typedef struct QuadCfg {
   int32_t env_kind;          /* QUAD_ENV_HOVER | QUAD_ENV_TRAJ */
-  int32_t wrapper;           /* QUAD_WRAP_NONE | QUAD_WRAP_CTBR (RateControlWrapper) */
+  int32_t wrapper;           /* QUAD_WRAP_NONE | _CTBR (RateControlWrapper) | _RELPOS | _CTBR_RELPOS */
   int32_t max_episode_steps; /* 512 hover / 2048 traj */
   int32_t auto_reset;        /* 1: SB3 VecEnv semantics (reset on terminated|truncated) */
   float obs_low[12], obs_high[12];       /* HoverEnv._obs_bounds   (normalization) */
@@ -146,7 +150,8 @@ int32_t quad_num_envs(const QuadHandle* h);
 /* Diagnostics: the step-kernel form quad_create chose -- bits 0-3 lanes per env (0 = one thread
  * per env; 1/2/4 = k_step_g), bit 4 set when the handle's constant block is a reference default and
  * the kernels with compiled-in constants run (QUADENV_SPEC=0 turns that off), bit 5 set when the
- * one-thread form runs with helper waves drawing the resets (k_step_h; QUADENV_HELPER=0 turns it off). */
+ * one-thread form runs with helper waves drawing the resets (k_step_h; QUADENV_HELPER=0 turns it off).
+ * 64 alone: a RELPOS or brax handle, whose one step kernel (k_step_relpos / k_step_brax) has no forms. */
 int32_t quad_kernel_form(const QuadHandle* h);
 
 /* Re-key the reset RNG (HoverEnv.reset(seed=...), hover_env.py:210 -> gymnasium seeding) and
@@ -369,7 +374,8 @@ typedef struct QuadPPOBatch {
   const float* returns;     /* [M] */
   const int64_t* index;     /* [batch] rows of this minibatch, each in [0, M) */
   int32_t batch;            /* >= 1 */
-  int32_t normalize_advantage;
+  int32_t normalize_advantage;  /* 0: off; 1: on; QUAD_ADV_PRECOMPUTED: on, and quad_ppo_adv_stats already
+                                   wrote this minibatch's sums into the same workspace (stream-ordered) */
   float clip_range, ent_coef, vf_coef;
   float* stats;             /* [4] out, or NULL: pg_loss, vf_loss, entropy, clip_fraction */
 } QuadPPOBatch;
@@ -411,6 +417,20 @@ int64_t quad_ppo_workspace_bytes(int32_t batch);
 int quad_ppo_grad_form(void);
 int quad_ppo_grad(const QuadPolicyParams* params, const QuadPPOBatch* b, const QuadPolicyGrads* grads,
                   void* workspace, int64_t workspace_bytes, void* stream);
+/* The minibatch advantage statistics quad_ppo_grad's normalization needs (sum, sum of squares,
+ * float64), on their own: a data-parallel learner enqueues them for the NEXT minibatch while the
+ * gradient all-reduce of this one is in flight (they read only advantages[index]), then calls
+ * quad_ppo_grad with normalize_advantage = QUAD_ADV_PRECOMPUTED and the same workspace. */
+enum { QUAD_ADV_PRECOMPUTED = 2 };
+int quad_ppo_adv_stats(const QuadPPOBatch* b, void* workspace, int64_t workspace_bytes, void* stream);
+/* Diagnostics (parity tests): quad_ppo_grad through a build of the same kernel body that also
+ * records the hidden pre-activations (before the ReLU) it computed for every minibatch row:
+ * hidden[(net * batch + pos) * 256 + 128 * layer + neuron], net 0 = actor / 1 = critic, pos = the
+ * row's position in `index`, layer 0 = h1 / 1 = h2 (device float32 [2][batch][256]). The gradients
+ * are written as by quad_ppo_grad. Lets a test count the kernel's own ReLU decisions against
+ * float64 (no reference interface: SB3 exposes no such hook). */
+int quad_ppo_hidden(const QuadPolicyParams* params, const QuadPPOBatch* b, const QuadPolicyGrads* grads,
+                    float* hidden, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

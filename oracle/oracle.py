@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "libquadoracle.so")
 
 ENV_HOVER, ENV_TRAJ, ENV_BRAX_HOVER, ENV_BRAX_TRAJ = 0, 1, 2, 3
-WRAP_NONE, WRAP_CTBR, WRAP_RELPOS = 0, 1, 2
+WRAP_NONE, WRAP_CTBR, WRAP_RELPOS, WRAP_CTBR_RELPOS = 0, 1, 2, 3
 
 
 class OracleOpt(C.Structure):
@@ -256,6 +256,10 @@ class Env:
     @property
     def qvel(self):
         return np.array(self.s.qvel[:], dtype=np.float64)
+
+    @property
+    def rate_int(self):
+        return np.array(self.s.rate_int[:], dtype=np.float64)
 
     def set_full_state(self, qpos, qvel, voltage, target, step_count, rate_int=(0, 0, 0),
                        state12=None, prev_action=(0, 0, 0, 0)):

@@ -679,7 +679,8 @@ int oracle_env_step(const OracleCfg* cfg, OracleEnv* env, const float action[4],
                     OracleStepOut* out) {
   float a[4];
   a[0] = action[0];
-  if (cfg->wrapper == ORACLE_WRAP_CTBR) { /* RateControlWrapper.action (rate_wrapper.py:69-98) */
+  const int ctbr = cfg->wrapper == ORACLE_WRAP_CTBR || cfg->wrapper == ORACLE_WRAP_CTBR_RELPOS;
+  if (ctbr) { /* RateControlWrapper.action (rate_wrapper.py:69-98) */
     const double dt = cfg->opt.timestep;
     for (int k = 0; k < 3; k++) {
       const double des = (double)action[1 + k] * cfg->rate_max_rad;
@@ -695,8 +696,9 @@ int oracle_env_step(const OracleCfg* cfg, OracleEnv* env, const float action[4],
   }
   memcpy(out->env_action, a, sizeof a);
   /* self._prev_action = np.array(action, dtype=np.float32) (hover_env.py:166): the action the
-   * base env receives (after RateControlWrapper.action when that wrapper is on) */
-  memcpy(env->prev_action, a, sizeof a);
+   * base env receives; RateControlWrapper.step then overwrites it with the rate action it was
+   * given (rate_wrapper.py:100-106), which is what RelPosActWrapper above it reads */
+  memcpy(env->prev_action, ctbr ? action : a, sizeof a);
   /* denormalize (normalization.py:20-30), float32 */
   float phys[4];
   for (int k = 0; k < 4; k++) {

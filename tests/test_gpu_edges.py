@@ -93,44 +93,58 @@ def test_termination_edges_through_step(golden_dir, env_name, key, kind):
     env.close()
 
 
-@pytest.mark.parametrize("name,env_name,kind,max_steps", [("relpos_steps", "hover", O.ENV_HOVER, 60),
-                                                         ("traj_relpos_steps", "trajectory", O.ENV_TRAJ, 50)])
-def test_relpos_step_matches_oracle_and_reference(golden_dir, name, env_name, kind, max_steps):
+RELPOS_KINDS = [("relpos_steps", "hover", O.ENV_HOVER, 60, "RelPosActWrapper", O.WRAP_RELPOS),
+                ("traj_relpos_steps", "trajectory", O.ENV_TRAJ, 50, "RelPosActWrapper", O.WRAP_RELPOS),
+                ("ctbr_relpos_steps", "hover", O.ENV_HOVER, 60, "ctbr_relpos", O.WRAP_CTBR_RELPOS),
+                ("traj_ctbr_relpos_steps", "trajectory", O.ENV_TRAJ, 50, "ctbr_relpos", O.WRAP_CTBR_RELPOS)]
+
+
+@pytest.mark.parametrize("name,env_name,kind,max_steps,wrapper,wrap", RELPOS_KINDS)
+def test_relpos_step_matches_oracle_and_reference(golden_dir, name, env_name, kind, max_steps, wrapper, wrap):
+    """RelPosActWrapper (and RelPosActWrapper(RateControlWrapper(.)), the README's stack) through
+    k_step_relpos from the reference's recorded states: oracle-parity and reference goldens."""
     d = np.load(os.path.join(golden_dir, f"golden_{name}.npz"))
     n = len(d["action"])
-    env = _env(n, env_name, "RelPosActWrapper", auto_reset=False, max_episode_steps=max_steps)
+    env = _env(n, env_name, wrapper, auto_reset=False, max_episode_steps=max_steps)
     st = dict(qpos=d["pre_qpos"].astype(np.float32), qvel=d["pre_qvel"].astype(np.float32),
               voltage=d["pre_voltage"].astype(np.float32), target=d["pre_target"],
-              step_count=d["pre_step"].astype(np.int32), prev_action=d["pre_prev_action"])
+              step_count=d["pre_step"].astype(np.int32), prev_action=d["pre_prev_action"],
+              rate_int=d["pre_rate_int"].astype(np.float32))
     env.set_state(**st)
     obs, rew, te, tr, inf = env.step(torch.from_numpy(d["action"]).cuda(), info="full")
     obs = obs.cpu().numpy(); te = te.cpu().numpy(); tr = tr.cpu().numpy(); rew = rew.cpu().numpy()
     assert obs.shape == (n, 7)
-    cfg = O.default_cfg(kind, O.WRAP_RELPOS)
+    cfg = O.default_cfg(kind, wrap)
     cfg.max_episode_steps = max_steps
     for i in range(n):
         e = O.Env(cfg=cfg)
         e.set_full_state(st["qpos"][i], st["qvel"][i], st["voltage"][i], st["target"][i], st["step_count"][i],
-                         (0, 0, 0), None, st["prev_action"][i])
+                         st["rate_int"][i], None, st["prev_action"][i])
         o = O.out_to_dict(e.step(d["action"][i]))
         assert te[i] == o["terminated"] == d["terminated"][i] and tr[i] == o["truncated"] == d["truncated"][i], i
         assert parity_ok(obs[i], o["obs7"]) and parity_ok(obs[i], d["obs"][i]), (i, obs[i], o["obs7"])
         assert np.array_equal(obs[i][3:], d["obs"][i][3:])  # the previous action is copied exactly
         assert parity_ok(rew[i], o["reward"]), i
+        if wrap == O.WRAP_CTBR_RELPOS:
+            assert parity_ok(inf["motor_commands"].cpu().numpy()[i], o["motor_commands"]), i
     g = env.get_state()
     assert np.array_equal(g["prev_action"], d["action"])
+    if wrap == O.WRAP_CTBR_RELPOS:
+        assert np.all(np.abs(g["rate_int"] - d["post_rate_int"]) <= 1e-5 * np.abs(d["post_rate_int"]) + 1e-9)
     env.close()
 
 
-@pytest.mark.parametrize("env_name,kind", [("hover", O.ENV_HOVER), ("trajectory", O.ENV_TRAJ)])
-def test_relpos_auto_reset_matches_oracle(env_name, kind):
+@pytest.mark.parametrize("env_name,kind,wrapper,wrap", [("hover", O.ENV_HOVER, "RelPosActWrapper", O.WRAP_RELPOS),
+                                                        ("trajectory", O.ENV_TRAJ, "RelPosActWrapper", O.WRAP_RELPOS),
+                                                        ("hover", O.ENV_HOVER, "ctbr_relpos", O.WRAP_CTBR_RELPOS)])
+def test_relpos_auto_reset_matches_oracle(env_name, kind, wrapper, wrap):
     """SB3 auto-reset under RelPosActWrapper: terminal_observation = the wrapper's obs7 of the
     finishing step (prev action = the action just taken); the returned obs = obs7 of the reset
     (Philox draws of the episode counter, prev action zeros), bit-exact with the oracle."""
     n = 4096
-    env = _env(n, env_name, "RelPosActWrapper", seed=31, max_episode_steps=7)
+    env = _env(n, env_name, wrapper, seed=31, max_episode_steps=7)
     env.reset()
-    cfg = O.default_cfg(kind, O.WRAP_RELPOS)
+    cfg = O.default_cfg(kind, wrap)
     cfg.max_episode_steps = 7
     checked = 0
     for k in range(16):
@@ -142,7 +156,7 @@ def test_relpos_auto_reset_matches_oracle(env_name, kind):
         for i in np.nonzero(te | tr)[0][:40]:
             e = O.Env(cfg=cfg)
             e.set_full_state(pre["qpos"][i], pre["qvel"][i], pre["voltage"][i], pre["target"][i],
-                             pre["step_count"][i], (0, 0, 0), None, pre["prev_action"][i])
+                             pre["step_count"][i], pre["rate_int"][i], None, pre["prev_action"][i])
             o = O.out_to_dict(e.step(a[i]))
             assert parity_ok(tobs[i], o["obs7"]) and np.array_equal(tobs[i][3:], a[i]), i
             i12, t3 = O.reset_draw(cfg, 31, i, pre["episode"][i])

@@ -133,6 +133,13 @@ def test_kernel_form_selection(spec_mode):
         e = _env(1024, env_name, wrapper)
         assert N.lib().quad_kernel_form(e._h) == 32 | (16 if spec_mode == "1" else 0), (env_name, wrapper)
         e.close()
+    # RELPOS and brax handles launch k_step_relpos / k_step_brax whatever their size: no form bits
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    for kw in (dict(env="hover", wrapper="RelPosActWrapper"), dict(env="trajectory", wrapper="RelPosActWrapper"),
+               dict(env="brax_hover"), dict(env="brax_jax_mjx")):
+        e = QuadVecEnv(1024, device="cuda:0", seed=0, **kw)
+        assert N.lib().quad_kernel_form(e._h) == 64, kw
+        e.close()
 
 
 @pytest.mark.parametrize("env_name,wrapper,kind,wrap", VARIANTS)

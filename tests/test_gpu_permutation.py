@@ -83,3 +83,39 @@ def test_seeded_and_near_uniform():
     dof = (n - 1) ** 2
     assert abs(chi2 - dof) < 6 * np.sqrt(2 * dof), (chi2, dof)
     assert N.lib().quad_permutation(0, 1, None, None) == N.QUAD_EINVAL
+
+
+@pytest.mark.parametrize("seed", [0, 7, 2**61 + 5])
+def test_config3_domain_statistics(seed):
+    """At config 3's own domain -- a 65,536 x 1,024 rollout buffer, n = 2^26 rows, 128 minibatches of
+    524,288 -- where the Feistel halves are 13 bits wide:
+      * the first minibatch's values are uniform over 1,024 equal value buckets (chi-square; the
+        sample is drawn without replacement, which only narrows the spread);
+      * consecutive outputs are uncorrelated (lag-1 serial correlation, |r| < 6 / sqrt(m));
+      * the minibatch touches as many distinct 4-KB pages of the [n, 12] float32 observation buffer
+        as uniform samples of the same size (torch.randperm) do: no gather locality bias."""
+    n, m = 1 << 26, 524288
+    p = _perm(n, seed)
+    first = p[:m]
+    # value buckets
+    counts = torch.bincount(first // (n // 1024), minlength=1024).double().cpu().numpy()
+    exp = m / 1024
+    chi2 = ((counts - exp) ** 2 / exp).sum()
+    dof = 1023
+    assert abs(chi2 - dof) < 6 * np.sqrt(2 * dof), (chi2, dof)
+    # lag-1 serial correlation over the whole epoch and over the first minibatch
+    for seq in (p, first):
+        x = seq.double()
+        x = (x - x.mean()) / x.std()
+        r = (x[:-1] * x[1:]).mean().item()
+        assert abs(r) < 6 / np.sqrt(x.numel()), r
+    # distinct 4-KB pages of the observation rows (48 B each) a minibatch gathers from
+    def pages(idx):
+        lo, hi = (idx * 48) // 4096, (idx * 48 + 47) // 4096
+        return int(torch.unique(torch.cat([lo, hi])).numel())
+    got = pages(first)
+    g = torch.Generator(device="cuda").manual_seed(seed & 0xFFFF)
+    uni = np.array([pages(torch.randperm(n, device="cuda", generator=g)[:m]) for _ in range(4)], dtype=np.float64)
+    print(f"\nseed {seed}: chi2 {chi2:.1f} (dof {dof}); distinct obs pages {got} vs uniform {uni.mean():.0f} "
+          f"+- {uni.std():.0f} of {n * 48 // 4096}")
+    assert abs(got - uni.mean()) <= max(6 * uni.std(), 1e-3 * uni.mean()), (got, uni)

@@ -91,3 +91,39 @@ def test_relpos_wrapper_facade():
     assert np.array_equal(obs[3:], a) and np.array_equal(env.observation(np.arange(12, dtype=np.float32))[3:], a)
     assert env.observation_space.shape == (7,)
     env.close()
+
+
+def test_relpos_over_rate_control_stack():
+    """The README's stack RelPosActWrapper(RateControlWrapper(HoverEnv())): the CTBR controller stays
+    in the step (combined kernel kind QUAD_WRAP_CTBR_RELPOS) and obs7 carries the rate action
+    (rate_wrapper.py:100-106); bit-identical to building that kind directly; wrapping keeps the
+    wrapped env's seed and cfg overrides; the reverse order is refused with an explanation."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    from uav_reinforcement_learning_control_amd.envs import (HoverEnv, QuadVecEnv, RateControlWrapper,
+                                                             RelPosActWrapper)
+    env = RelPosActWrapper(RateControlWrapper(HoverEnv(device="cuda:0", seed=7, density=0.9), kd=[20, 20, 10]))
+    assert isinstance(env.env, RateControlWrapper) and env.observation_space.shape == (7,)
+    cfg = env.unwrapped._vec.cfg
+    assert cfg.wrapper == N.WRAP_CTBR_RELPOS and abs(cfg.density - 0.9) < 1e-12
+    np.testing.assert_allclose(cfg.rate_kd[:], [20, 20, 10])
+    assert env.unwrapped._vec.seed_value == 7
+    obs, _ = env.reset(seed=2)
+    assert obs.shape == (7,) and np.all(obs[3:] == 0)
+    a = np.array([0.1, 0.4, -0.3, 0.2], np.float32)
+    obs, *_ = env.step(a)
+    assert np.array_equal(obs[3:], a)                         # the RATE action, not the torques
+    assert np.any(env.env._rate_int_torque != 0)              # the controller ran
+    env.close()
+    # vectorized: the facade stack steps exactly the combined kind
+    n = 512
+    w = RelPosActWrapper(RateControlWrapper(QuadVecEnv(n, device="cuda:0", seed=4)))
+    d = QuadVecEnv(n, wrapper="ctbr_relpos", device="cuda:0", seed=4)
+    assert torch.equal(w.reset(), d.reset())
+    for k in range(6):
+        acts = d.random_actions(k)
+        o1 = w.step(acts)[0].clone()
+        o2 = d.step(acts)[0]
+        assert torch.equal(o1, o2) and torch.equal(o2[:, 3:], acts)
+    w.close(); d.close()
+    with pytest.raises(TypeError):
+        RateControlWrapper(RelPosActWrapper(HoverEnv(device="cuda:0")))

@@ -85,20 +85,28 @@ def test_termination_matches_reference(golden_dir):
             assert mine == bool(t)
 
 
-@pytest.mark.parametrize("name,kind", [("relpos_steps", O.ENV_HOVER), ("traj_relpos_steps", O.ENV_TRAJ)])
-def test_relpos_wrapper_matches_reference(golden_dir, name, kind):
+@pytest.mark.parametrize("name,kind,wrap", [("relpos_steps", O.ENV_HOVER, O.WRAP_RELPOS),
+                                             ("traj_relpos_steps", O.ENV_TRAJ, O.WRAP_RELPOS),
+                                             ("ctbr_relpos_steps", O.ENV_HOVER, O.WRAP_CTBR_RELPOS),
+                                             ("traj_ctbr_relpos_steps", O.ENV_TRAJ, O.WRAP_CTBR_RELPOS)])
+def test_relpos_wrapper_matches_reference(golden_dir, name, kind, wrap):
     """RelPosActWrapper(HoverEnv / TrajectoryFollowEnv) (envs/wrappers.py:13-25), the reference's
     wrapper executed unmodified: obs7 = [obs12[0:3], _prev_action] bit-exact for every step (the
-    previous action is the one just taken) and every reset (zeros, hover_env.py:212)."""
+    previous action is the one just taken) and every reset (zeros, hover_env.py:212). The
+    *_ctbr_relpos fixtures are RelPosActWrapper(RateControlWrapper(env)) (the README's stack): the
+    rate controller's torques drive the step and obs7 carries the RATE action (rate_wrapper.py:105)."""
     d = np.load(os.path.join(golden_dir, f"golden_{name}.npz"))
-    cfg = O.default_cfg(kind, O.WRAP_RELPOS)
+    cfg = O.default_cfg(kind, wrap)
     cfg.max_episode_steps = 60 if kind == O.ENV_HOVER else 50
     env = O.Env(cfg=cfg)
     for t in range(len(d["action"])):
         env.set_full_state(d["pre_qpos"][t], d["pre_qvel"][t], d["pre_voltage"][t], d["pre_target"][t],
-                           d["pre_step"][t], (0, 0, 0), d["pre_state12"][t], d["pre_prev_action"][t])
+                           d["pre_step"][t], d["pre_rate_int"][t], d["pre_state12"][t], d["pre_prev_action"][t])
         o = O.out_to_dict(env.step(d["action"][t]))
         assert np.array_equal(o["obs7"], d["obs"][t]), (name, t)
+        if wrap == O.WRAP_CTBR_RELPOS:
+            np.testing.assert_allclose(env.rate_int, d["post_rate_int"][t], rtol=1e-12, atol=1e-15)
+            np.testing.assert_allclose(o["motor_commands"], d["motor"][t], rtol=1e-13, atol=1e-13)
         assert o["terminated"] == d["terminated"][t] and o["truncated"] == d["truncated"][t]
         np.testing.assert_allclose(o["reward"], d["reward"][t], rtol=1e-13, atol=1e-15)
     assert d["terminated"].any() or d["truncated"].any()

@@ -125,8 +125,9 @@ def termination_fixture():
 
 def rollout_fixture(kind: str, wrapper, n_steps: int, seeds, max_episode_steps=None,
                     action_mode="mixed"):
-    """wrapper: False/None, True (RateControlWrapper) or "relpos" (RelPosActWrapper: the recorded
-    obs / reset_obs are then the wrapper's 7-D observations, plus pre_prev_action)."""
+    """wrapper: False/None, True (RateControlWrapper), "relpos" (RelPosActWrapper: the recorded
+    obs / reset_obs are then the wrapper's 7-D observations, plus pre_prev_action) or "ctbr_relpos"
+    (RelPosActWrapper(RateControlWrapper(env)), the stack the reference README documents)."""
     from envs.hover_env import HoverEnv
     from envs.rate_wrapper import RateControlWrapper
     from envs.trajectory_follow_env import TrajectoryFollowEnv
@@ -134,9 +135,14 @@ def rollout_fixture(kind: str, wrapper, n_steps: int, seeds, max_episode_steps=N
 
     kw = {} if max_episode_steps is None else dict(max_episode_steps=max_episode_steps)
     base = HoverEnv(**kw) if kind == "hover" else TrajectoryFollowEnv(**kw)
-    relpos = wrapper == "relpos"
-    env = RelPosActWrapper(base) if relpos else RateControlWrapper(base) if wrapper else base
-    wrapper = bool(wrapper) and not relpos  # the CTBR integrator fields below
+    relpos = wrapper in ("relpos", "ctbr_relpos")
+    if wrapper == "ctbr_relpos":
+        ctbr_env = RateControlWrapper(base)
+        env = RelPosActWrapper(ctbr_env)
+    else:
+        env = RelPosActWrapper(base) if relpos else RateControlWrapper(base) if wrapper else base
+        ctbr_env = env
+    wrapper = bool(wrapper) and wrapper != "relpos"  # the CTBR integrator fields below
     u = env.unwrapped
     arng = np.random.default_rng(99)
     rec = {k: [] for k in ("pre_qpos", "pre_qvel", "pre_voltage", "pre_target", "pre_step",
@@ -195,7 +201,7 @@ def rollout_fixture(kind: str, wrapper, n_steps: int, seeds, max_episode_steps=N
         rec["pre_target"].append(u.target_state.position.copy())
         rec["pre_step"].append(u._step_count)
         rec["pre_state12"].append(u._state.vec())
-        rec["pre_rate_int"].append(env._rate_int_torque.copy() if wrapper else np.zeros(3))
+        rec["pre_rate_int"].append(ctbr_env._rate_int_torque.copy() if wrapper else np.zeros(3))
         rec["pre_prev_action"].append(u._prev_action.copy())
         rec["action"].append(a)
         obs, r, te, tr, info = env.step(a)
@@ -210,7 +216,7 @@ def rollout_fixture(kind: str, wrapper, n_steps: int, seeds, max_episode_steps=N
         rec["post_qpos"].append(u.data.qpos.copy())
         rec["post_qvel"].append(u.data.qvel.copy())
         rec["post_state12"].append(u._state.vec())
-        rec["post_rate_int"].append(env._rate_int_torque.copy() if wrapper else np.zeros(3))
+        rec["post_rate_int"].append(ctbr_env._rate_int_torque.copy() if wrapper else np.zeros(3))
         if te or tr:
             do_reset(seeds.pop(0) if seeds else None)
     out = {k: np.array(v) for k, v in rec.items()}
@@ -247,7 +253,11 @@ def main():
                 "golden_relpos_steps.npz": lambda: rollout_fixture("hover", "relpos", 400, range(4000, 4100),
                                                                    max_episode_steps=60),
                 "golden_traj_relpos_steps.npz": lambda: rollout_fixture("traj", "relpos", 300, range(5000, 5100),
-                                                                        max_episode_steps=50)}
+                                                                        max_episode_steps=50),
+                "golden_ctbr_relpos_steps.npz": lambda: rollout_fixture("hover", "ctbr_relpos", 400,
+                                                                        range(6000, 6100), max_episode_steps=60),
+                "golden_traj_ctbr_relpos_steps.npz": lambda: rollout_fixture("traj", "ctbr_relpos", 300,
+                                                                             range(7000, 7100), max_episode_steps=50)}
         for name in args.only.split(","):
             d = lazy[name]()
             np.savez_compressed(os.path.join(args.out, name), **d)
@@ -268,6 +278,10 @@ def main():
         "golden_relpos_steps.npz": rollout_fixture("hover", "relpos", 400, range(4000, 4100), max_episode_steps=60),
         "golden_traj_relpos_steps.npz": rollout_fixture("traj", "relpos", 300, range(5000, 5100),
                                                         max_episode_steps=50),
+        "golden_ctbr_relpos_steps.npz": rollout_fixture("hover", "ctbr_relpos", 400, range(6000, 6100),
+                                                        max_episode_steps=60),
+        "golden_traj_ctbr_relpos_steps.npz": rollout_fixture("traj", "ctbr_relpos", 300, range(7000, 7100),
+                                                             max_episode_steps=50),
     }
     for name, d in fx.items():
         path = os.path.join(args.out, name)

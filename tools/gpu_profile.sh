@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 evidence for one round: kernel-trace stats of bench.py, then separate --pmc passes
-# (FETCH_SIZE, WRITE_SIZE) on bench.py and on the dword-copy calibration kernel.
+# (FETCH_SIZE, WRITE_SIZE) per step kernel via tools/pmc/traffic_round.sh.
 # Any step that faults / aborts / times out ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -19,10 +19,6 @@ run() {
 # >64 MiB trace); PMC passes on a minimal driver (tools/step_once.py: eager quad_step launches)
 B="python bench.py --no-cpu-baseline --e2e-iters 0 --steps 400 --warmup 100"
 run trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- $B
-for N in 65536 1048576; do
-  run pmc_fetch_$N 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch/$N -o step -- python tools/step_once.py $N 100
-  run pmc_write_$N 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write/$N -o step -- python tools/step_once.py $N 100
-done
-run pmc_cal_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_cal_fetch -o cal -- tools/pmc/_build/pmc_calib
-run pmc_cal_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_cal_write -o cal -- tools/pmc/_build/pmc_calib
+# HBM-side traffic per kernel: tools/pmc/traffic_round.sh (then tools/pmc/traffic_summary.py here)
+run traffic 900 bash tools/pmc/traffic_round.sh
 echo "=== done"

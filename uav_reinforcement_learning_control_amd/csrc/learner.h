@@ -40,6 +40,7 @@ struct GArgs {
   int32_t batch, nb, per_block;     // actor: nb blocks of per_block rows
   int32_t nbc, per_block_c;         // critic: nbc blocks of per_block_c rows
   float clip, inv_batch, vf_coef;
+  float* dump;  // diagnostics only (k_ppo_grad*_dump): [2 nets][batch][256] hidden pre-activations
 };
 
 struct Layout {
@@ -68,6 +69,14 @@ inline Layout layout_of(int32_t batch, int actor_share) {
 // the bf16x3 form (learner_x3.hip): its actor share and launcher
 int x3_actor_share();
 int launch_ppo_grad_x3(const GArgs& g, hipStream_t s);
+int launch_ppo_grad_x3_dump(const GArgs& g, hipStream_t s);
+
+// Diagnostics (quad_ppo_hidden): the kernels' own hidden pre-activations of minibatch row `pos`
+// (before the ReLU; layer 0 = h1, 1 = h2) -- the dump instantiation of the same body, so the same
+// arithmetic as the gradient launch
+__device__ __forceinline__ void dump_pre(float* dump, int net, int batch, int pos, int layer, int neuron, float v) {
+  dump[(size_t(net) * size_t(batch) + size_t(pos)) * 256 + size_t(128 * layer + neuron)] = v;
+}
 
 }  // namespace lrn
 }  // namespace quadenv

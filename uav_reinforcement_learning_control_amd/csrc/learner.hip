@@ -72,7 +72,7 @@ __device__ __forceinline__ int kperm(int s, int h) { return 4 * (s >> 1) + 2 * h
 
 __device__ __forceinline__ float2 ld2(const float* L, int off) { return *reinterpret_cast<const float2*>(L + off); }
 
-template <int NOUT>
+template <int NOUT, bool DUMP = false>
 __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int blk) {
   const NetW& W = NOUT == ACT ? g.actor : g.critic;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
@@ -199,6 +199,10 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
 #pragma unroll
       for (int s = 0; s < 6; s++)
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1f[s], OBSI[(32 * t + l32) * SO + 2 * s + h], acc, 0, 0, 0);
+      if constexpr (DUMP) {
+        if (valid[t])
+          for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 0, 32 * w + acc_row(r, h), acc[r]);
+      }
       float* row = L + L_H1 + (32 * t + l32) * SH + 32 * w;
 #pragma unroll
       for (int r = 0; r < 16; r += 2)  // rows acc_row(r), acc_row(r)+1 are adjacent neurons
@@ -222,6 +226,11 @@ __device__ __forceinline__ void body(const GArgs& g, float* __restrict__ L, int 
       }
     }
 #endif
+    if constexpr (DUMP) {
+      for (int t = 0; t < 2; t++)
+        if (valid[t])
+          for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 1, 32 * w + acc_row(r, h), h2[t][r]);
+    }
     // head partial sums over the wave's 32 neurons (the two lane halves hold 16 each)
     float part[2][NOUT];
 #pragma unroll
@@ -419,6 +428,12 @@ __global__ __launch_bounds__(LB, 1) void k_ppo_grad(GArgs g) {
   extern __shared__ float lds[];
   if (int(blockIdx.x) < g.nb) body<ACT>(g, lds, blockIdx.x);
   else body<1>(g, lds, blockIdx.x - g.nb);
+}
+
+__global__ __launch_bounds__(LB, 1) void k_ppo_grad_dump(GArgs g) {
+  extern __shared__ float lds_d[];
+  if (int(blockIdx.x) < g.nb) body<ACT, true>(g, lds_d, blockIdx.x);
+  else body<1, true>(g, lds_d, blockIdx.x - g.nb);
 }
 
 // minibatch sums of adv and adv^2 in float64 (fixed order: per-thread strided, then a tree)
@@ -632,8 +647,13 @@ int quad_ppo_grad_form(void) {
   return (v && std::strcmp(v, "f32") == 0) ? 0 : 1;
 }
 
-int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPolicyGrads* gr, void* workspace,
-                  int64_t workspace_bytes, void* stream) {
+}  // extern "C"
+
+namespace {
+// quad_ppo_grad, or (dump != NULL: quad_ppo_hidden) the dump instantiation of the same gradient
+// kernel, which also records every minibatch row's hidden pre-activations
+int ppo_grad_impl(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPolicyGrads* gr, void* workspace,
+                  int64_t workspace_bytes, void* stream, float* dump) {
   if (!p || !b || !gr || !workspace) return lfail(QUAD_EINVAL, "NULL argument");
   if (!p->pi_w0 || !p->pi_b0 || !p->pi_w1 || !p->pi_b1 || !p->act_w || !p->act_b || !p->vf_w0 || !p->vf_b0 ||
       !p->vf_w1 || !p->vf_b1 || !p->val_w || !p->val_b || !p->log_std)
@@ -650,6 +670,7 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   if (!(b->clip_range > 0.f)) return lfail(QUAD_EINVAL, "clip_range must be > 0");
   const bool x3 = quad_ppo_grad_form() == 1;
   const Layout l = layout_of(b->batch, x3 ? x3_actor_share() : ACTOR_SHARE);
+  if (dump && int64_t(b->batch) * 2 * 256 * 4 > (int64_t(1) << 40)) return lfail(QUAD_EINVAL, "batch too large to dump");
   if (workspace_bytes < l.adv_bytes + l.part_bytes) return lfail(QUAD_EINVAL, "workspace too small");
   static bool opted[64] = {};
   int dev = 0;
@@ -657,6 +678,8 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   const int lds_bytes = L_TOTAL * int(sizeof(float));
   if (!x3 && !opted[dev]) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds_bytes) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_dump), hipFuncAttributeMaxDynamicSharedMemorySize,
                             lds_bytes) != hipSuccess)
       return lfail(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     opted[dev] = true;
@@ -665,7 +688,7 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   double* adv_part = static_cast<double*>(workspace);
   float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) + l.adv_bytes);
   const bool norm = b->normalize_advantage && b->batch > 1;
-  if (norm) {
+  if (norm && b->normalize_advantage != QUAD_ADV_PRECOMPUTED) {  // (2: quad_ppo_adv_stats ran for this batch)
     hipLaunchKernelGGL(k_adv_stats, dim3(ADV_BLOCKS), dim3(256), 0, s, b->advantages, b->index, b->batch, adv_part);
     if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_adv_stats launch failed");
   }
@@ -679,8 +702,12 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   g.part = part;
   g.batch = b->batch; g.nb = l.nb; g.per_block = l.per_block; g.nbc = l.nbc; g.per_block_c = l.per_block_c;
   g.clip = b->clip_range; g.inv_batch = 1.0f / float(b->batch); g.vf_coef = b->vf_coef;
+  g.dump = dump;
   if (x3) {
-    if (int rc = launch_ppo_grad_x3(g, s)) return rc;
+    if (int rc = dump ? launch_ppo_grad_x3_dump(g, s) : launch_ppo_grad_x3(g, s)) return rc;
+  } else if (dump) {
+    hipLaunchKernelGGL(k_ppo_grad_dump, dim3(l.nb + l.nbc), dim3(LB), lds_bytes, s, g);
+    if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_grad_dump launch failed");
   } else {
     hipLaunchKernelGGL(k_ppo_grad, dim3(l.nb + l.nbc), dim3(LB), lds_bytes, s, g);
     if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_grad launch failed");
@@ -691,6 +718,32 @@ int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   hipLaunchKernelGGL(k_ppo_reduce, dim3((2 * PSTRIDE + 255) / 256), dim3(256), 0, s, r);
   if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_reduce launch failed");
   return QUAD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int quad_ppo_grad(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPolicyGrads* gr, void* workspace,
+                  int64_t workspace_bytes, void* stream) {
+  return ppo_grad_impl(p, b, gr, workspace, workspace_bytes, stream, nullptr);
+}
+
+int quad_ppo_adv_stats(const QuadPPOBatch* b, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!b || !workspace || !b->advantages || !b->index) return lfail(QUAD_EINVAL, "NULL argument");
+  if (b->batch < 1) return lfail(QUAD_EINVAL, "batch must be >= 1");
+  const Layout l = layout_of(b->batch, ACTOR_SHARE);
+  if (workspace_bytes < l.adv_bytes + l.part_bytes) return lfail(QUAD_EINVAL, "workspace too small");
+  if (b->batch > 1)
+    hipLaunchKernelGGL(k_adv_stats, dim3(ADV_BLOCKS), dim3(256), 0, static_cast<hipStream_t>(stream), b->advantages,
+                       b->index, b->batch, static_cast<double*>(workspace));
+  if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_adv_stats launch failed");
+  return QUAD_OK;
+}
+
+int quad_ppo_hidden(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPolicyGrads* gr, float* hidden,
+                    void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!hidden) return lfail(QUAD_EINVAL, "hidden is NULL");
+  return ppo_grad_impl(p, b, gr, workspace, workspace_bytes, stream, hidden);
 }
 
 int quad_permutation(int64_t n, uint64_t seed, int64_t* out, void* stream) {

@@ -177,7 +177,7 @@ __device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, s16x8(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)));
 }
 
-template <int NOUT>
+template <int NOUT, bool DUMP = false>
 __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int blk) {
   const NetW& W = NOUT == ACT ? g.actor : g.critic;
   float* const Lf = reinterpret_cast<float*>(L);
@@ -337,6 +337,10 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
       for (int p = 0; p < 3; p++) xb.p[p] = rd16(XO, p * XIMG + (32 * t + l32) * XROW + 16 * h);
       acc = mma3(w1x, xb, acc);
+      if constexpr (DUMP) {
+        if (valid[t])
+          for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 0, 32 * w + acc_row(r, h), acc[r]);
+      }
 #pragma unroll
       for (int gg = 0; gg < 4; gg++) {  // registers 4gg.. = neurons 32w + 8gg + 4h + 0..3
         const float v[4] = {relu(acc[4 * gg]), relu(acc[4 * gg + 1]), relu(acc[4 * gg + 2]), relu(acc[4 * gg + 3])};
@@ -381,6 +385,11 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     f32x16 h2[2];
     for (int r = 0; r < 16; r++) { h2[0][r] = Lf[r]; h2[1][r] = Lf[r + 16]; }
 #endif
+    if constexpr (DUMP) {
+      for (int t = 0; t < 2; t++)
+        if (valid[t])
+          for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 1, 32 * w + acc_row(r, h), h2[t][r]);
+    }
     // head partial sums over the wave's 32 neurons (the two lane halves hold 16 each)
 #pragma unroll
     for (int t = 0; t < 2; t++) {
@@ -648,6 +657,13 @@ __global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3(GArgs g) {
   else body<1>(g, lds_x3, blockIdx.x - g.nb);
 }
 
+// diagnostics: the same body with the hidden pre-activations recorded (quad_ppo_hidden)
+__global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3_dump(GArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds_x3d[];
+  if (int(blockIdx.x) < g.nb) body<ACT, true>(g, lds_x3d, blockIdx.x);
+  else body<1, true>(g, lds_x3d, blockIdx.x - g.nb);
+}
+
 // one net per kernel (QUADENV_LEARNER_SPLIT=1): each gets its own register allocation; the two
 // launch on two streams (fork / join by events) so their blocks share the chip
 template <int NOUT>
@@ -703,6 +719,15 @@ int launch_ppo_grad_x3(const GArgs& g, hipStream_t s) {
   }
   hipLaunchKernelGGL(k_ppo_grad_x3, dim3(g.nb + g.nbc), dim3(LB), B_TOTAL, s, g);
   if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3 launch failed");
+  return QUAD_OK;
+}
+
+int launch_ppo_grad_x3_dump(const GArgs& g, hipStream_t s) {
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_x3_dump), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          B_TOTAL) != hipSuccess)
+    return set_error(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  hipLaunchKernelGGL(k_ppo_grad_x3_dump, dim3(g.nb + g.nbc), dim3(LB), B_TOTAL, s, g);
+  if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3_dump launch failed");
   return QUAD_OK;
 }
 

@@ -57,6 +57,10 @@ int fail(int code, const std::string& msg) {
 int hip_fail(hipError_t e, const char* what) {
   return fail(QUAD_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
+// wrapper kinds: the RelPosActWrapper output stage (obs7) and the CTBR action path
+inline bool wrap_relpos(int32_t w) { return w == QUAD_WRAP_RELPOS || w == QUAD_WRAP_CTBR_RELPOS; }
+inline bool wrap_ctbr(int32_t w) { return w == QUAD_WRAP_CTBR || w == QUAD_WRAP_CTBR_RELPOS; }
+
 #define HIP_TRY(expr)                                  \
   do {                                                 \
     hipError_t e__ = (expr);                           \
@@ -642,22 +646,24 @@ __global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __r
 // RelPosActWrapper (envs/wrappers.py:13-25) around HoverEnv / TrajectoryFollowEnv: the same step,
 // emitting obs7 = [obs[0:3], _prev_action] where _prev_action is the action just taken
 // (hover_env.py:166) and zeros after a reset (:212). The previous action is kept in the SoA
-// (F_PREV) so quad_observe / get_state stay exact.
-template <int KIND>
+// (F_PREV) so quad_observe / get_state stay exact. CTBR: RelPosActWrapper(RateControlWrapper(env))
+// -- the action is the rate command the controller maps to torques, and it is also what the
+// obs7 carries (rate_wrapper.py:100-106 overwrites _prev_action with it after the base step).
+template <int KIND, bool CTBR>
 __global__ __launch_bounds__(BLOCK) void k_step_relpos(const KConsts<float>* __restrict__ kc, KParams p,
                                                        const float4* __restrict__ act, QuadStepOut out) {
   p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
   const int i = p.first + blockIdx.x * BLOCK + threadIdx.x;
   if (i >= p.first + p.count) return;
   EnvRegs<float> e;
-  load_env(p, i, e, false);
+  load_env(p, i, e, CTBR);
   const Tiles S(p);
   const uint32_t vo = env_off(uint32_t(i));
   const uint32_t ep = S.ldu(F_EP, vo);
   const float4 a4 = act[i];
   const float a[4] = {a4.x, a4.y, a4.z, a4.w};
   StepRes r;
-  env_step<float, false>(*p.kc, e, a, r);
+  env_step<float, CTBR>(*p.kc, e, a, r);
   float info[9];
   if (out.target_info) target_info_of<KIND>(*p.kc, p, i, e, ep, info);
   float o7[7] = {r.obs[0], r.obs[1], r.obs[2], a[0], a[1], a[2], a[3]};
@@ -687,7 +693,7 @@ __global__ __launch_bounds__(BLOCK) void k_step_relpos(const KConsts<float>* __r
 #pragma unroll
     for (int j = 0; j < 4; j++) { o7[3 + j] = 0.f; prev[j] = 0.f; }
   }
-  store_env(p, i, e, false);
+  store_env(p, i, e, CTBR);
 #pragma unroll
   for (int j = 0; j < 4; j++) S.st(F_PREV + j, vo, prev[j]);
 #pragma unroll
@@ -1473,7 +1479,7 @@ int quad_default_cfg(int32_t env_kind, int32_t wrapper, QuadCfg* c) {
   if (!c) return fail(QUAD_EINVAL, "cfg is NULL");
   if (env_kind < QUAD_ENV_HOVER || env_kind > QUAD_ENV_BRAX_TRAJ)
     return fail(QUAD_EINVAL, "unknown env_kind");
-  if (wrapper < QUAD_WRAP_NONE || wrapper > QUAD_WRAP_RELPOS) return fail(QUAD_EINVAL, "unknown wrapper");
+  if (wrapper < QUAD_WRAP_NONE || wrapper > QUAD_WRAP_CTBR_RELPOS) return fail(QUAD_EINVAL, "unknown wrapper");
   if (env_kind >= QUAD_ENV_BRAX_HOVER && wrapper != QUAD_WRAP_NONE)
     return fail(QUAD_EINVAL, "the brax env kinds take no wrapper");
   default_cfg_fill(env_kind, wrapper, c);
@@ -1490,7 +1496,7 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
     return fail(QUAD_EINVAL, "n_envs too large (max 31,580,608)");
   if (cfg->env_kind < QUAD_ENV_HOVER || cfg->env_kind > QUAD_ENV_BRAX_TRAJ)
     return fail(QUAD_EINVAL, "unknown env_kind");
-  if (cfg->wrapper < QUAD_WRAP_NONE || cfg->wrapper > QUAD_WRAP_RELPOS)
+  if (cfg->wrapper < QUAD_WRAP_NONE || cfg->wrapper > QUAD_WRAP_CTBR_RELPOS)
     return fail(QUAD_EINVAL, "unknown wrapper");
   if (cfg->env_kind >= QUAD_ENV_BRAX_HOVER && cfg->wrapper != QUAD_WRAP_NONE)
     return fail(QUAD_EINVAL, "the brax env kinds take no wrapper");
@@ -1559,7 +1565,11 @@ void quad_destroy(QuadHandle* h) {
 int32_t quad_num_envs(const QuadHandle* h) { return h ? h->n : 0; }
 
 int32_t quad_kernel_form(const QuadHandle* h) {
-  return h ? (h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0)) : -1;
+  if (!h) return -1;
+  // RELPOS and the brax kinds have one kernel each (k_step_relpos / k_step_brax): no lanes, SPEC
+  // or helper forms to report
+  if (wrap_relpos(h->cfg.wrapper) || h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) return 64;
+  return h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0);
 }
 
 int quad_seed(QuadHandle* h, uint64_t seed, void* stream) {
@@ -1580,9 +1590,9 @@ int quad_reset(QuadHandle* h, const uint8_t* mask, float* obs, void* stream) {
     hipLaunchKernelGGL(k_reset_brax<QUAD_ENV_BRAX_HOVER>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
   else if (h->cfg.env_kind == QUAD_ENV_BRAX_TRAJ)
     hipLaunchKernelGGL(k_reset_brax<QUAD_ENV_BRAX_TRAJ>, dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
-  else if (h->cfg.wrapper == QUAD_WRAP_RELPOS && h->cfg.env_kind == QUAD_ENV_TRAJ)
+  else if (wrap_relpos(h->cfg.wrapper) && h->cfg.env_kind == QUAD_ENV_TRAJ)
     hipLaunchKernelGGL((k_reset<QUAD_ENV_TRAJ, true>), dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
-  else if (h->cfg.wrapper == QUAD_WRAP_RELPOS)
+  else if (wrap_relpos(h->cfg.wrapper))
     hipLaunchKernelGGL((k_reset<QUAD_ENV_HOVER, true>), dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
   else if (h->cfg.env_kind == QUAD_ENV_TRAJ)
     hipLaunchKernelGGL((k_reset<QUAD_ENV_TRAJ, false>), dim3(grid_of(h->n)), dim3(BLOCK), 0, s, h->kp, mask, obs);
@@ -1617,12 +1627,17 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
   KParams kp = h->kp;
   kp.first = first;
   kp.count = count;
-  if (h->cfg.wrapper == QUAD_WRAP_RELPOS) {
+  if (wrap_relpos(h->cfg.wrapper)) {
     const dim3 grid(grid_of(count));
-    if (traj)
-      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_TRAJ>), grid, blk, 0, s, h->kdev, kp, a, *out);
+    const bool rc = h->cfg.wrapper == QUAD_WRAP_CTBR_RELPOS;
+    if (traj && rc)
+      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_TRAJ, true>), grid, blk, 0, s, h->kdev, kp, a, *out);
+    else if (traj)
+      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_TRAJ, false>), grid, blk, 0, s, h->kdev, kp, a, *out);
+    else if (rc)
+      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_HOVER, true>), grid, blk, 0, s, h->kdev, kp, a, *out);
     else
-      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_HOVER>), grid, blk, 0, s, h->kdev, kp, a, *out);
+      hipLaunchKernelGGL((k_step_relpos<QUAD_ENV_HOVER, false>), grid, blk, 0, s, h->kdev, kp, a, *out);
   } else if (h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) {
     const dim3 grid(grid_of(count));
     if (h->cfg.env_kind == QUAD_ENV_BRAX_TRAJ)
@@ -1693,7 +1708,7 @@ int quad_rollout(QuadHandle* h, const float* packed, const QuadRollout* r, void*
     return fail(QUAD_EINVAL, "quad_rollout: packed, actions, obs_copy and last_obs must be 16-byte aligned");
   if (h->cfg.env_kind != QUAD_ENV_HOVER && h->cfg.env_kind != QUAD_ENV_TRAJ)
     return fail(QUAD_EINVAL, "quad_rollout: env_kind must be HOVER or TRAJ");
-  if (h->cfg.wrapper == QUAD_WRAP_RELPOS) return fail(QUAD_EINVAL, "quad_rollout: the policy takes 12-D obs (no RELPOS)");
+  if (wrap_relpos(h->cfg.wrapper)) return fail(QUAD_EINVAL, "quad_rollout: the policy takes 12-D obs (no RELPOS)");
   if (!h->cfg.auto_reset) return fail(QUAD_EINVAL, "quad_rollout: the handle needs auto_reset = 1");
   DeviceGuard g(h->device);
   RollArgs a{r->obs_copy, r->actions, r->log_prob, r->value, r->episode_starts, r->rewards, r->last_obs,
@@ -1714,7 +1729,7 @@ int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream) {
     HIP_TRY(hipGetLastError());
     return QUAD_OK;
   }
-  if (h->cfg.wrapper == QUAD_WRAP_RELPOS)
+  if (wrap_relpos(h->cfg.wrapper))
     hipLaunchKernelGGL(k_observe<true>, dim3(grid_of(h->n)), dim3(BLOCK), 0, static_cast<hipStream_t>(stream),
                        h->kp, obs, state12);
   else
@@ -1731,7 +1746,7 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
   if (steps == 0) return QUAD_OK;
   if (h->cfg.env_kind != QUAD_ENV_HOVER && h->cfg.env_kind != QUAD_ENV_TRAJ)
     return fail(QUAD_EINVAL, "quad_step_random drives the hover / trajectory kinds");
-  if (h->cfg.wrapper == QUAD_WRAP_RELPOS) return fail(QUAD_EINVAL, "quad_step_random: wrapper NONE or CTBR");
+  if (wrap_relpos(h->cfg.wrapper)) return fail(QUAD_EINVAL, "quad_step_random: wrapper NONE or CTBR");
   if (!out->obs || !out->reward || !out->terminated || !out->truncated)
     return fail(QUAD_EINVAL, "obs, reward, terminated and truncated are required");
   if (out->motor_commands || out->voltage_scale || out->state12 || out->target_info)
@@ -1859,7 +1874,7 @@ int quad_waypoints_begin(QuadHandle* h, const QuadWaypoints* w, const QuadWaypoi
   if (!obs) return fail(QUAD_EINVAL, "obs is NULL");
   DeviceGuard g(h->device);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (h->cfg.wrapper == QUAD_WRAP_RELPOS)
+  if (wrap_relpos(h->cfg.wrapper))
     hipLaunchKernelGGL(k_waypoints_begin<true>, dim3(grid_of(h->n)), dim3(BLOCK), 0, st, h->kp, *w, *s, obs);
   else
     hipLaunchKernelGGL(k_waypoints_begin<false>, dim3(grid_of(h->n)), dim3(BLOCK), 0, st, h->kp, *w, *s, obs);

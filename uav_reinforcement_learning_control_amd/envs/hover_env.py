@@ -39,6 +39,7 @@ class HoverEnv:
     def __init__(self, render_mode: Optional[str] = None, max_episode_steps: Optional[int] = None,
                  device=None, wrapper: Optional[str] = None, seed: int = 0, **cfg_overrides):
         self.render_mode = render_mode
+        self._seed, self._overrides = int(seed), dict(cfg_overrides)  # (wrappers rebuild with them)
         self._vec = QuadVecEnv(1, env=self._KIND, wrapper=wrapper, device=device, seed=seed,
                                max_episode_steps=max_episode_steps, auto_reset=False,
                                cfg_overrides=cfg_overrides or None)

@@ -14,6 +14,22 @@ from .hover_env import HoverEnv
 from .vec_env import QuadVecEnv
 
 
+def rebuild(env, wrapper: str, extra: Optional[dict] = None):
+    """A copy of `env` (a QuadVecEnv or a HoverEnv / TrajectoryFollowEnv facade) with the kernel's
+    wrapper kind `wrapper`: same size, device, seed, env ids, episode length, auto-reset and
+    cfg overrides (+ `extra`), so wrapping never changes the dynamics or bounds of a customized env."""
+    if isinstance(env, QuadVecEnv):
+        return QuadVecEnv(env.num_envs, env=env.env_kind, wrapper=wrapper, device=env.device,
+                          seed=env.seed_value, env_id_base=env.env_id_base,
+                          max_episode_steps=env.max_episode_steps, auto_reset=bool(env.cfg.auto_reset),
+                          cfg_overrides={**env.cfg_overrides, **(extra or {})})
+    if isinstance(env, HoverEnv):
+        return type(env)(render_mode=env.render_mode, max_episode_steps=env.max_episode_steps,
+                         device=env._vec.device, wrapper=wrapper, seed=env._seed,
+                         **{**env._overrides, **(extra or {})})
+    raise TypeError(f"cannot wrap {type(env).__name__}")
+
+
 def _gain_overrides(max_rate, kd, ki_rate_torque, integral_max):
     o = {}
     if max_rate is not None:
@@ -25,6 +41,10 @@ def _gain_overrides(max_rate, kd, ki_rate_torque, integral_max):
     if integral_max is not None:
         o["rate_imax"] = float(integral_max)
     return o
+
+
+def _wrapper_of(env):
+    return env.wrapper if isinstance(env, QuadVecEnv) else env._vec.wrapper
 
 
 class RateControlWrapper:
@@ -43,18 +63,11 @@ class RateControlWrapper:
     def __init__(self, env, max_rate: Optional[float] = None, kd=None,
                  ki_rate_torque: Optional[float] = None, integral_max: Optional[float] = None):
         o = _gain_overrides(max_rate, kd, ki_rate_torque, integral_max)
-        if isinstance(env, QuadVecEnv):
-            inner = QuadVecEnv(env.num_envs, env=env.env_kind, wrapper="RateControlWrapper",
-                               device=env.device, seed=env.seed_value, env_id_base=env.env_id_base,
-                               max_episode_steps=env.max_episode_steps,
-                               auto_reset=bool(env.cfg.auto_reset), cfg_overrides=o)
-            cfg = inner.cfg
-        elif isinstance(env, HoverEnv):
-            inner = type(env)(render_mode=env.render_mode, max_episode_steps=env.max_episode_steps,
-                              device=env._vec.device, wrapper="RateControlWrapper", **o)
-            cfg = inner._vec.cfg
-        else:
-            raise TypeError(f"cannot wrap {type(env).__name__}")
+        if isinstance(env, (QuadVecEnv, HoverEnv)) and _wrapper_of(env) not in (None, "none"):
+            raise TypeError("RateControlWrapper wraps the bare env; stack RelPosActWrapper on top of it "
+                            "(RelPosActWrapper(RateControlWrapper(env)), as the reference README does)")
+        inner = rebuild(env, "RateControlWrapper", o)
+        cfg = inner.cfg if isinstance(inner, QuadVecEnv) else inner._vec.cfg
         env.close()
         self.env = inner
         self._single = not isinstance(inner, QuadVecEnv)

@@ -32,7 +32,9 @@ _ENV_KINDS = {"hover": N.ENV_HOVER, "HoverEnv": N.ENV_HOVER,
               "brax_jax_mjx": N.ENV_BRAX_TRAJ, "jax_mjx_quad": N.ENV_BRAX_TRAJ,
               "JaxMJXQuadBraxEnv": N.ENV_BRAX_TRAJ}
 _WRAPPERS = {None: N.WRAP_NONE, "none": N.WRAP_NONE, "RateControlWrapper": N.WRAP_CTBR,
-             "ctbr": N.WRAP_CTBR, "RelPosActWrapper": N.WRAP_RELPOS, "relpos": N.WRAP_RELPOS}
+             "ctbr": N.WRAP_CTBR, "RelPosActWrapper": N.WRAP_RELPOS, "relpos": N.WRAP_RELPOS,
+             # RelPosActWrapper(RateControlWrapper(env)), the stack the reference README documents
+             "RelPosActWrapper(RateControlWrapper)": N.WRAP_CTBR_RELPOS, "ctbr_relpos": N.WRAP_CTBR_RELPOS}
 
 
 def _ptr(t: Optional[torch.Tensor]):
@@ -61,6 +63,7 @@ class QuadVecEnv:
         self.wrapper = wrapper if wrapper not in (None, "none") else None
         self.seed_value = int(seed)
         self.env_id_base = int(env_id_base)
+        self.cfg_overrides = dict(cfg_overrides or {})  # kept so a wrapper can rebuild the same env
         L = N.lib()
         cfg = N.default_cfg(_ENV_KINDS[env], _WRAPPERS[wrapper])
         if max_episode_steps is not None:
@@ -82,7 +85,7 @@ class QuadVecEnv:
         self._h = h
         self.action_space = Box(-1.0, 1.0, (4,), np.float32)
         self.brax = cfg.env_kind >= N.ENV_BRAX_HOVER
-        self.obs_dim = 21 if self.brax else (7 if cfg.wrapper == N.WRAP_RELPOS else 12)
+        self.obs_dim = 21 if self.brax else (7 if cfg.wrapper in (N.WRAP_RELPOS, N.WRAP_CTBR_RELPOS) else 12)
         self.observation_space = (Box(-np.inf, np.inf, (21,), np.float32) if self.brax
                                   else Box(-1.0, 1.0, (self.obs_dim,), np.float32))
         n, dev = self.num_envs, self.device

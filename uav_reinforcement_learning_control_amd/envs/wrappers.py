@@ -13,26 +13,27 @@ class RelPosActWrapper:
 
     The observation is produced by the step kernel's output stage (QuadCfg.wrapper =
     QUAD_WRAP_RELPOS, k_step_relpos): wrapping rebuilds `env` (a QuadVecEnv or a HoverEnv /
-    TrajectoryFollowEnv facade) with that wrapper kind, so step/reset already return obs7.
+    TrajectoryFollowEnv facade) with that wrapper kind -- same seed, env ids and cfg overrides --
+    so step/reset already return obs7. Wrapping a RateControlWrapper (the README's
+    RelPosActWrapper(RateControlWrapper(HoverEnv())) stack) rebuilds the env under it with the
+    combined kind QUAD_WRAP_CTBR_RELPOS: the rate controller stays in the step and obs7 carries the
+    rate action (rate_wrapper.py:100-106); `env` is then that RateControlWrapper.
     `observation(obs12)` is the reference's mapping, for callers that apply it themselves."""
 
     def __init__(self, env):
         from ..utils.spaces import Box
-        from .hover_env import HoverEnv
-        from .vec_env import QuadVecEnv
-        if isinstance(env, QuadVecEnv):
-            inner = QuadVecEnv(env.num_envs, env=env.env_kind, wrapper="RelPosActWrapper", device=env.device,
-                               seed=env.seed_value, env_id_base=env.env_id_base,
-                               max_episode_steps=env.max_episode_steps, auto_reset=bool(env.cfg.auto_reset))
-        elif isinstance(env, HoverEnv):
-            inner = type(env)(render_mode=env.render_mode, max_episode_steps=env.max_episode_steps,
-                              device=env._vec.device, wrapper="RelPosActWrapper")
+        from .rate_wrapper import rebuild
+        if isinstance(env, RateControlWrapper):
+            old = env.env
+            env.env = rebuild(old, "ctbr_relpos")  # gains travel in the cfg overrides
+            old.close()
+            self.env = env
         else:
-            raise TypeError(f"cannot wrap {type(env).__name__}")
-        env.close()
-        self.env = inner
+            inner = rebuild(env, "RelPosActWrapper")
+            env.close()
+            self.env = inner
         self.observation_space = Box(-1.0, 1.0, (7,), np.float32)
-        self.action_space = inner.action_space
+        self.action_space = self.env.action_space
 
     def __getattr__(self, name):
         if name == "env":

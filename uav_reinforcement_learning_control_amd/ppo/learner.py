@@ -57,11 +57,33 @@ class FusedLearner:
         return (N.QuadPolicyParams(*[p.data_ptr() for p in ps]),
                 N.QuadPolicyGrads(*[p.grad.data_ptr() for p in ps]))
 
+    def _workspace(self, B: int) -> None:
+        need = int(self._lib.quad_ppo_workspace_bytes(B))
+        if self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+
+    def adv_stats(self, advantages: torch.Tensor, index: torch.Tensor) -> None:
+        """Enqueue the advantage statistics of minibatch `index` (quad_ppo_adv_stats) into the
+        workspace the next grads(..., adv_ready=True) reads; nothing else may run grads in between."""
+        if not self.normalize_advantage:
+            return
+        B = int(index.numel())
+        self._workspace(B)
+        b = N.QuadPPOBatch(0, 0, 0, advantages.data_ptr(), 0, index.data_ptr(), B, 1, 0.2, 0.0, 0.0, None)
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        N.check(self._lib.quad_ppo_adv_stats(C.byref(b), C.c_void_p(self._ws.data_ptr()), C.c_int64(self._ws.numel()),
+                                             stream), "quad_ppo_adv_stats")
+
     def grads(self, obs: torch.Tensor, actions: torch.Tensor, log_prob: torch.Tensor, advantages: torch.Tensor,
-              returns: torch.Tensor, index: torch.Tensor, stats: Optional[torch.Tensor] = None) -> None:
+              returns: torch.Tensor, index: torch.Tensor, stats: Optional[torch.Tensor] = None,
+              hidden: Optional[torch.Tensor] = None, adv_ready: bool = False) -> None:
         """Overwrite every parameter's .grad with the gradient of the PPO loss on rows `index` of the
         flattened buffers (obs [M,12], actions [M,4], log_prob / advantages / returns [M]).
-        `stats` (float32 [4], optional) receives pg_loss, vf_loss, entropy, clip_fraction."""
+        `stats` (float32 [4], optional) receives pg_loss, vf_loss, entropy, clip_fraction.
+        `hidden` (float32 [2, B, 256], diagnostics): run the kernel's dump build (quad_ppo_hidden),
+        which also records each row's hidden pre-activations [net][pos][h1 | h2].
+        `adv_ready`: adv_stats(advantages, index) was already enqueued for this minibatch (the
+        data-parallel overlap), so the launch sequence skips its own statistics pre-pass."""
         dev = self.device
         M = obs.shape[0]
         _need(obs, (M, 12), torch.float32, dev, "obs")
@@ -75,15 +97,22 @@ class FusedLearner:
             raise ValueError("empty minibatch")
         if stats is not None:
             _need(stats, (4,), torch.float32, dev, "stats")
-        need = int(self._lib.quad_ppo_workspace_bytes(B))
-        if self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        self._workspace(B)
         prm, grd = self._structs()
+        norm = int(self.normalize_advantage)
+        if norm and adv_ready:
+            norm = N.QUAD_ADV_PRECOMPUTED
         b = N.QuadPPOBatch(obs.data_ptr(), actions.data_ptr(), log_prob.data_ptr(), advantages.data_ptr(),
-                           returns.data_ptr(), index.data_ptr(), B, int(self.normalize_advantage),
+                           returns.data_ptr(), index.data_ptr(), B, norm,
                            self.clip_range, self.ent_coef, self.vf_coef,
                            None if stats is None else stats.data_ptr())
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        if hidden is not None:
+            _need(hidden, (2, B, 256), torch.float32, dev, "hidden")
+            N.check(self._lib.quad_ppo_hidden(C.byref(prm), C.byref(b), C.byref(grd), C.c_void_p(hidden.data_ptr()),
+                                              C.c_void_p(self._ws.data_ptr()), C.c_int64(self._ws.numel()), stream),
+                    "quad_ppo_hidden")
+            return
         N.check(self._lib.quad_ppo_grad(C.byref(prm), C.byref(b), C.byref(grd), C.c_void_p(self._ws.data_ptr()),
                                         C.c_int64(self._ws.numel()), stream), "quad_ppo_grad")
 

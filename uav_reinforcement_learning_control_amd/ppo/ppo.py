@@ -109,18 +109,14 @@ def _bucket_bound(params, flat: torch.Tensor) -> bool:
     return True
 
 
-def _rccl_has_avg() -> bool:
-    """ncclAvg exists from NCCL 2.10 (RCCL follows the NCCL API versions)."""
-    try:
-        return tuple(torch.cuda.nccl.version()[:2]) >= (2, 10)
-    except Exception:
-        return False
-
-
-def allreduce_mean_(params, flat: torch.Tensor, world: int) -> None:
-    """Average the gradients of `params` over ranks with ONE all_reduce of a flat fp32 bucket.
-    With the .grad tensors bound to the bucket (bind_grad_bucket) the collective runs in place;
-    otherwise (a caller replaced a .grad) they are copied in and out."""
+def allreduce_mean_(params, flat: torch.Tensor, world: int, between: Optional[Callable[[], None]] = None) -> None:
+    """Average the gradients of `params` over ranks with ONE all_reduce of a flat fp32 bucket:
+    SUM, then a division by the world size -- the same two ops on RCCL and on gloo, so the gloo
+    tests exercise exactly what the GPU job runs. With the .grad tensors bound to the bucket
+    (bind_grad_bucket) the collective runs in place; otherwise (a caller replaced a .grad) they are
+    copied in and out. `between`, if given, is called while the collective is in flight (it must
+    not touch the bucket): on RCCL its launches overlap the all-reduce (work.wait() only makes the
+    current stream wait on the communication stream)."""
     bound = _bucket_bound(params, flat)
     if not bound:
         off = 0
@@ -128,11 +124,11 @@ def allreduce_mean_(params, flat: torch.Tensor, world: int) -> None:
             k = p.numel()
             flat[off:off + k].copy_(p.grad.reshape(-1))
             off += k
-    if dist.get_backend() == "nccl" and _rccl_has_avg():
-        dist.all_reduce(flat, op=dist.ReduceOp.AVG)   # RCCL: the mean in the collective itself
-    else:
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM)   # gloo has no AVG
-        flat.div_(world)
+    work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True)
+    if between is not None:
+        between()
+    work.wait()
+    flat.div_(world)
     if not bound:
         off = 0
         for p in params:
@@ -398,19 +394,27 @@ class PPO:
         total = obs.shape[0]
         steps = epochs * nmb if max_minibatches is None else min(epochs * nmb, max_minibatches)
         mstats = torch.zeros(max(steps, 1), 4, dtype=torch.float32, device=self.device)
+        perms = {}
+
+        def index_of(k):  # the k-th minibatch of the update: epoch k // nmb, slot k % nmb
+            e, m = divmod(k, nmb)
+            if e not in perms:  # drawn in epoch order, as the per-epoch loop drew them
+                perms[e] = epoch_permutation(total, self.device)
+            return perms[e][m * B:(m + 1) * B]
+
+        # data-parallel: the next minibatch's advantage statistics (they read only adv[index])
+        # run while this minibatch's gradient all-reduce is in flight
+        overlap = self.world > 1 and cfg.normalize_advantage
         done = 0
-        for _ in range(epochs):
-            if done >= steps:
-                break
-            perm = epoch_permutation(total, self.device)
-            for m in range(nmb):
-                if done >= steps:
-                    break
-                self._learner.grads(obs, act, logp_old, adv, ret, perm[m * B:(m + 1) * B], mstats[done])
-                if self.world > 1:
-                    allreduce_mean_(self.params, self._flat, self.world)
-                self._adam.step()  # clip_grad_norm_ + Adam.step (quad_clip_adam)
-                done += 1
+        for k in range(steps):
+            idx = index_of(k)
+            self._learner.grads(obs, act, logp_old, adv, ret, idx, mstats[k], adv_ready=overlap and k > 0)
+            if self.world > 1:
+                nxt = (lambda: self._learner.adv_stats(adv, index_of(k + 1))) if overlap and k + 1 < steps else None
+                allreduce_mean_(self.params, self._flat, self.world, between=nxt)
+            self._adam.step()  # clip_grad_norm_ + Adam.step (quad_clip_adam)
+            perms.pop(k // nmb - 1, None)
+            done += 1
         a = mstats[:done].double().mean(0).tolist() if done else [0.0] * 4
         stats.update(pg_loss=a[0], vf_loss=a[1], entropy=a[2], clip_fraction=a[3], n=done)
         return stats
