@@ -281,34 +281,55 @@ def _end_to_end(env, args, world: int = 1) -> dict:
 
 
 def _learner_kernel(m) -> dict:
-    """quad_ppo_grad alone on the rollout buffer (one minibatch of the SB3 schedule), HIP-event
-    timed on its stream: the MFMA roofline of the update. FLOP = the issued 32x32x2 / 16x16x4
-    products per row (L1, L2, dW2, dh1, dW1 + the dW3 16x16x4) for both nets."""
+    """quad_ppo_grad alone on the rollout buffer, over consecutive minibatches of the training's own
+    epoch permutation (ppo.epoch_permutation -> quad_permutation, as PPO.train draws them),
+    HIP-event timed on its stream: the MFMA roofline of the update. Also the whole fused optimizer
+    step (quad_ppo_grad + quad_clip_adam) over the same minibatches, to set beside the end-to-end
+    ms_per_optimizer_step (which adds the host loop). FLOP = the issued products per row."""
+    from uav_reinforcement_learning_control_amd.ppo.ppo import epoch_permutation
     total = m.buf_obs.shape[0] * m.buf_obs.shape[1]
     obs, act = m.buf_obs.view(total, -1), m.buf_act.view(total, 4)
     lp, adv, ret = m.buf_logp.view(total), m.buf_adv.view(total), m.buf_ret.view(total)
-    idx = torch.randperm(total, device=obs.device)[:m.batch].contiguous()
-    m._learner.grads(obs, act, lp, adv, ret, idx)
+    perm = epoch_permutation(total, obs.device)
+    B = m.batch
+    nmb = max(1, total // B)
+    reps = min(20, nmb)
+    idx = [perm[k * B:(k + 1) * B] for k in range(reps)]
+    m._learner.grads(obs, act, lp, adv, ret, idx[0])
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 20
     e0.record()
-    for _ in range(reps):
-        m._learner.grads(obs, act, lp, adv, ret, idx)
+    for k in range(reps):
+        m._learner.grads(obs, act, lp, adv, ret, idx[k])
     e1.record()
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
+    saved = [p.detach().clone() for p in m.params]  # (the optimizer steps below are undone)
+    saved_opt = {k: {n: (t.clone() if torch.is_tensor(t) else t) for n, t in v.items()} for k, v in m.opt.state.items()}
+    e0.record()
+    for k in range(reps):
+        m._learner.grads(obs, act, lp, adv, ret, idx[k])
+        m._adam.step()
+    e1.record()
+    torch.cuda.synchronize()
+    us_step = e0.elapsed_time(e1) * 1e3 / reps
+    with torch.no_grad():
+        for p, q in zip(m.params, saved):
+            p.copy_(q)
+    for k, v in saved_opt.items():
+        m.opt.state[k].update(v)
     # the f32 algorithm's MFMA work per row per net: (12 + 128 + 128 + 128 + 32) 32x32x2 per 64 rows
     # per wave x 4 waves, plus 32 16x16x4 (half the cycles) -> 444 x 2048 x 2 flop x 4 / 64 rows
-    flop = 2 * m.batch * (444 * 2048 * 2 * 4 / 64)
+    flop = 2 * B * (444 * 2048 * 2 * 4 / 64)
     from uav_reinforcement_learning_control_amd import _native as N
     form = int(N.lib().quad_ppo_grad_form())
     out = {"kernel": "quad_ppo_grad (k_adv_stats + %s + k_ppo_reduce)" % ("k_ppo_grad_x3" if form else "k_ppo_grad"),
-           "rows": m.batch, "us_per_minibatch": us, "issued_flop": flop}
+           "rows": B, "index_source": "epoch_permutation (quad_permutation), consecutive minibatches",
+           "us_per_minibatch": us, "us_per_optimizer_step_device": us_step, "issued_flop": flop}
     if form:
         # bf16x3: per 64-row round and wave 336 v_mfma_f32_32x32x16_bf16 (32 cycles each: L1 12, L2 96,
         # dW2 96 + db2 12, dh1 96, dW1 24) + 32 f32 16x16x4 (dW3, 32 cycles each)
-        cyc = 2 * (m.batch / 64) * 4 * (336 * 32 + 32 * 32) / 1024  # per SIMD, both nets
+        cyc = 2 * (B / 64) * 4 * (336 * 32 + 32 * 32) / 1024  # per SIMD, both nets
         floor_us = cyc / 2.4e3  # at the 2.4 GHz peak clock
         out.update({"f32_equivalent_TFLOPs": flop / us / 1e6, "peak_TFLOPs": 157.3,
                     "f32_equivalent_frac": flop / us / 1e6 / 157.3,

@@ -122,8 +122,9 @@ def test_relpos_over_rate_control_stack():
     for k in range(6):
         acts = d.random_actions(k)
         o1 = w.step(acts)[0].clone()
-        o2 = d.step(acts)[0]
-        assert torch.equal(o1, o2) and torch.equal(o2[:, 3:], acts)
+        o2, _, te, tr, _ = d.step(acts)
+        live = ~(te | tr)  # (auto-reset rows carry the reset obs: previous action zeros)
+        assert torch.equal(o1, o2) and torch.equal(o2[live][:, 3:], acts[live])
     w.close(); d.close()
     with pytest.raises(TypeError):
         RateControlWrapper(RelPosActWrapper(HoverEnv(device="cuda:0")))

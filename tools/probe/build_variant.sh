@@ -11,6 +11,6 @@ while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   ( /opt/rocm/bin/hipcc $F -I$O $flags -c -o ../../tools/_build/obj/quadenv_var_$name.o quadenv.hip &&
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_build/var_$name.so \
-      ../../tools/_build/obj/quadenv_var_$name.o $O/policy.o $O/rollout.o $O/learner.o ) &
+      ../../tools/_build/obj/quadenv_var_$name.o $O/policy.o $O/rollout.o $O/learner.o $O/learner_x3.o ) &
 done
 wait

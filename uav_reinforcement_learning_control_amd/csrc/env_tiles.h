@@ -99,6 +99,28 @@ __device__ __forceinline__ void load_env(const KParams& p, int i, EnvRegs<float>
   e.step = int32_t(S.ldu(F_STEP, o));
 }
 
+// the fields the physics and the observation need (not the voltage / CTBR integral: k_step_h's
+// helper waves own the control path)
+__device__ __forceinline__ void load_env_motion(const KParams& p, int i, EnvRegs<float>& e) {
+  const Tiles S(p);
+  const uint32_t o = env_off(uint32_t(i));
+#pragma unroll
+  for (int j = 0; j < 3; j++) e.pos[j] = S.ld(F_QPOS + j, o);
+#pragma unroll
+  for (int j = 0; j < 4; j++) e.q[j] = S.ld(F_QPOS + 3 + j, o);
+#pragma unroll
+  for (int j = 0; j < 4; j++) e.th[j] = S.ld(F_QPOS + 7 + j, o);
+#pragma unroll
+  for (int j = 0; j < 3; j++) e.v[j] = S.ld(F_QVEL + j, o);
+#pragma unroll
+  for (int j = 0; j < 3; j++) e.w[j] = S.ld(F_QVEL + 3 + j, o);
+#pragma unroll
+  for (int j = 0; j < 4; j++) e.s[j] = S.ld(F_QVEL + 6 + j, o);
+#pragma unroll
+  for (int j = 0; j < 3; j++) e.target[j] = S.ld(F_TGT + j, o);
+  e.step = int32_t(S.ldu(F_STEP, o));
+}
+
 __device__ __forceinline__ void store_env(const KParams& p, int i, const EnvRegs<float>& e,
                                           bool ctbr) {
   const Tiles S(p);

@@ -355,34 +355,42 @@ QD_HD void box_drag(const T w[3], const T u[3], const T kqa[3], const T kva, con
   }
 }
 
-// qacc of the free base + 4 props at (q, v, w, s, th) under the motor wrench (total thrust
-// along base z and torque about the base origin, base frame). Outputs: vdot (world),
-// wdot (body), sdot[4].
+// qacc of the free base + 4 props at (q, v, w, s, th) under the motor wrench, in two parts so
+// that the part which does not depend on the controls can run before (or beside) them:
+//   forward_base:   R = quat2mat(q), and the external force (base frame) / torque about the base
+//                   origin (base frame) of gravity, the base inertia-box drag and the 4 prop drags,
+//                   accumulated from zero in that order; the props' spin-axis drag torques Qs
+//   forward_finish: + the motor wrench (total thrust along base z, torque), velocity products,
+//                   3x3 solve -> vdot (world), wdot (body), sdot[4]
+// Every step form (k_step, k_step_h, k_step_random*, k_step_relpos, k_rollout) calls both in
+// this order, so they compute the same bits whichever wave runs the control path.
 template <typename T>
-QD_HD void forward_acc(const PhysConsts<T>& c, const T qn[4], const T th[4], const T v[3],
-                       const T w[3], const T s[4], const T Fsum, const T taum[3], T vdot[3],
-                       T wdot[3], T sdot[4]) {
+struct ForceAcc {
+  T R[9];
+  T FB[3], tau[3], Qs[4];
+};
+
+template <typename T>
+QD_HD void forward_base(const PhysConsts<T>& c, const T qn[4], const T th[4], const T v[3], const T w[3],
+                        const T s[4], ForceAcc<T>& o) {
   // R = quat2mat(q) (q already normalized)
   const T qw = qn[0], qx = qn[1], qy = qn[2], qz = qn[3];
-  T R[9];
+  T* R = o.R;
   R[0] = T(1) - T(2) * (qy * qy + qz * qz); R[1] = T(2) * (qx * qy - qw * qz); R[2] = T(2) * (qx * qz + qw * qy);
   R[3] = T(2) * (qx * qy + qw * qz); R[4] = T(1) - T(2) * (qx * qx + qz * qz); R[5] = T(2) * (qy * qz - qw * qx);
   R[6] = T(2) * (qx * qz - qw * qy); R[7] = T(2) * (qy * qz + qw * qx); R[8] = T(1) - T(2) * (qx * qx + qy * qy);
   T vB[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) vB[i] = R[i] * v[0] + R[3 + i] * v[1] + R[6 + i] * v[2];
-
-  // total external force (base frame) and torque about the base origin (base frame)
-  T FB[3] = {T(0), T(0), Fsum};
-  T tau[3] = {taum[0], taum[1], taum[2]};
+  T* FB = o.FB;
+  T* tau = o.tau;
   // gravity on every body COM: M g at cbar
   {
     const T mg = c.mt * c.gz;
     const T gB[3] = {mg * R[6], mg * R[7], mg * R[8]};
-    T t[3];
-    cross(c.cbar, gB, t);
+    cross(c.cbar, gB, tau);
 #pragma unroll
-    for (int i = 0; i < 3; i++) { FB[i] += gB[i]; tau[i] += t[i]; }
+    for (int i = 0; i < 3; i++) FB[i] = gB[i];
   }
   // base fluid: body frame == principal frame, COM at the origin
   {
@@ -394,7 +402,7 @@ QD_HD void forward_acc(const PhysConsts<T>& c, const T qn[4], const T th[4], con
   // prop fluid: prop frame = base frame rotated by th_i about z; COM on the axis at pc_i
   // (written as explicit fma chains: -ffp-contract=on fuses only within one expression, and the
   // cross products, frame rotations and accumulations below are ~1/3 of the physics)
-  T Qs[4];
+  T* Qs = o.Qs;
 #if defined(QD_ABL_NOPROPS)  // cost ablation (tools only): no prop drag terms
   Qs[0] = Qs[1] = Qs[2] = Qs[3] = T(0);
   if (false)
@@ -419,6 +427,43 @@ QD_HD void forward_acc(const PhysConsts<T>& c, const T qn[4], const T th[4], con
     tau[2] = q_fma(r[0], f[1], q_fma(-r[1], f[0], tau[2] + tp[2]));
     Qs[p] = tp[2];
   }
+}
+
+// The motor wrench of mj_fwdActuation for ctrl F (site transmission; float64 -> T): total thrust
+// along base z and the torque about the base origin. `zero`: MuJoCo's bad-ctrl / bad-state
+// handling zeroes every ctrl. F_NONNEG: the caller guarantees F >= 0 (or -0, or NaN) -- env_step's
+// F * vs -- so the ctrlrange clamp's lower bound (drone.xml's fixed 0, quad_model.h) cannot bind.
+template <typename T>
+struct Wrench {
+  T Fsum, taum[3];
+};
+template <typename T, bool F_NONNEG>
+QD_HD Wrench<T> wrench_of(const PhysConsts<T>& c, const double Fin[4], bool zero) {
+  double F[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double f = zero ? 0.0 : Fin[i];
+    if (F_NONNEG)  // ctrl_lo <= 0 <= f: only the upper bound can bind
+      F[i] = f > c.ctrl_hi ? c.ctrl_hi : f;
+    else
+      F[i] = clipn(f, c.ctrl_lo, c.ctrl_hi);  // flat selects; a NaN ctrl (CHECKS = false, the brax
+                                              // kinds: mjx has no bad-ctrl zeroing) passes through
+  }
+  Wrench<T> wr;
+  wr.Fsum = T(F[0] + F[1] + F[2] + F[3]);
+  wr.taum[0] = T(c.syd[0] * F[0] + c.syd[1] * F[1] + c.syd[2] * F[2] + c.syd[3] * F[3]);
+  wr.taum[1] = T(-(c.sxd[0] * F[0] + c.sxd[1] * F[1] + c.sxd[2] * F[2] + c.sxd[3] * F[3]));
+  wr.taum[2] = T(c.g5d[0] * F[0] + c.g5d[1] * F[1] + c.g5d[2] * F[2] + c.g5d[3] * F[3]);
+  return wr;
+}
+
+template <typename T>
+QD_HD void forward_finish(const PhysConsts<T>& c, const ForceAcc<T>& a, const T w[3], const T s[4],
+                          const Wrench<T>& m, T vdot[3], T wdot[3], T sdot[4]) {
+  const T* R = a.R;
+  const T FB[3] = {a.FB[0], a.FB[1], a.FB[2] + m.Fsum};
+  const T tau[3] = {a.tau[0] + m.taum[0], a.tau[1] + m.taum[1], a.tau[2] + m.taum[2]};
+  const T* Qs = a.Qs;
   // velocity-product (bias) terms
   T wc[3], wwc[3];
   cross(w, c.cbar, wc);
@@ -464,56 +509,30 @@ QD_HD void normalize4(T q[4]) {
   }
 }
 
-template <typename T, bool CHECKS, bool F_NONNEG>
-QD_HD void physics_body(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4], bool bad);
-
-// mujoco.mj_step for one env. Fin: ctrl in float64 (may be NaN / out of range; MuJoCo semantics).
-// CHECKS = false: mjx.step semantics (the brax kinds): no bad-state / bad-ctrl / bad-acc resets,
-// NaN propagates.
-// F_NONNEG: the caller guarantees Fin >= 0 (or -0, or NaN) -- env_step's F * vs -- so the
-// ctrlrange clamp's lower bound (drone.xml's fixed 0, quad_model.h) cannot bind and is skipped.
-// (A speculative form -- step first, screen the loaded state afterwards -- measured slower.)
-template <typename T, bool CHECKS = true, bool F_NONNEG = false>
-QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4]) {
-  // mj_checkPos / mj_checkVel: bad state => mj_resetData (qpos0, zero qvel, zero ctrl)
+// mj_checkPos / mj_checkVel: a bad state (NaN / Inf / |x| > 1e10) is reset to qpos0 with zero
+// qvel (mj_resetData); returns whether it was
+template <typename T>
+QD_HD bool check_state(EnvRegs<T>& e) {
   const T st[21] = {e.pos[0], e.pos[1], e.pos[2], e.q[0], e.q[1], e.q[2], e.q[3], e.th[0], e.th[1], e.th[2], e.th[3],
                     e.v[0], e.v[1], e.v[2], e.w[0], e.w[1], e.w[2], e.s[0], e.s[1], e.s[2], e.s[3]};
-  physics_body<T, CHECKS, F_NONNEG>(c, e, Fin, CHECKS ? any_bad(st) : false);
-}
-
-template <typename T, bool CHECKS, bool F_NONNEG>
-QD_HD void physics_body(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4], bool bad) {
-  bool badctrl = false;
-#pragma unroll
-  for (int i = 0; i < 4; i++) badctrl |= isbad(Fin[i]);
-  if (!CHECKS) bad = badctrl = false;
+  const bool bad = any_bad(st);
   if (bad) {
 #pragma unroll
     for (int i = 0; i < 3; i++) { e.pos[i] = T(0); e.v[i] = T(0); e.w[i] = T(0); }
     e.q[0] = T(1); e.q[1] = e.q[2] = e.q[3] = T(0);
 #pragma unroll
     for (int i = 0; i < 4; i++) { e.th[i] = T(0); e.s[i] = T(0); }
-    badctrl = true;
   }
-  // mj_fwdActuation: bad ctrl => all ctrl zeroed; ctrlrange clamp; site-transmission wrench
-  double F[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const double f = badctrl ? 0.0 : Fin[i];
-    if (F_NONNEG)  // ctrl_lo <= 0 <= f: only the upper bound can bind
-      F[i] = f > c.ctrl_hi ? c.ctrl_hi : f;
-    else
-      F[i] = clipn(f, c.ctrl_lo, c.ctrl_hi);  // flat selects; a NaN ctrl (CHECKS = false, the brax
-                                              // kinds: mjx has no bad-ctrl zeroing) passes through
-  }
-  T Fsum = T(F[0] + F[1] + F[2] + F[3]);
-  T taum[3] = {T(c.syd[0] * F[0] + c.syd[1] * F[1] + c.syd[2] * F[2] + c.syd[3] * F[3]),
-               T(-(c.sxd[0] * F[0] + c.sxd[1] * F[1] + c.sxd[2] * F[2] + c.sxd[3] * F[3])),
-               T(c.g5d[0] * F[0] + c.g5d[1] * F[1] + c.g5d[2] * F[2] + c.g5d[3] * F[3])};
-  T qn[4] = {e.q[0], e.q[1], e.q[2], e.q[3]};
-  normalize4(qn);
+  return bad;
+}
+
+// the rest of mj_step once the state is checked and the wrench known: forward_finish,
+// mj_checkAcc, mj_Euler (semi-implicit), MuJoCo's quaternion integration
+template <typename T, bool CHECKS>
+QD_HD void physics_finish(const PhysConsts<T>& c, EnvRegs<T>& e, T qn[4], const ForceAcc<T>& fa,
+                          const Wrench<T>& m) {
   T vdot[3], wdot[3], sdot[4];
-  forward_acc(c, qn, e.th, e.v, e.w, e.s, Fsum, taum, vdot, wdot, sdot);
+  forward_finish(c, fa, e.w, e.s, m, vdot, wdot, sdot);
   const T acc[10] = {vdot[0], vdot[1], vdot[2], wdot[0], wdot[1], wdot[2], sdot[0], sdot[1], sdot[2], sdot[3]};
   const bool badacc = any_bad(acc);
   if (CHECKS && badacc) {  // mj_checkAcc: reset to qpos0 with zero ctrl; at rest there the only force is
@@ -561,6 +580,32 @@ QD_HD void physics_body(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
   e.q[1] = a0 * qr[1] + a1 * qr[0] + a2 * qr[3] - a3 * qr[2];
   e.q[2] = a0 * qr[2] - a1 * qr[3] + a2 * qr[0] + a3 * qr[1];
   e.q[3] = a0 * qr[3] + a1 * qr[2] - a2 * qr[1] + a3 * qr[0];
+}
+
+template <typename T>
+QD_HD bool any_bad_ctrl(const double F[4]) {
+  bool b = false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) b |= isbad(F[i]);
+  return b;
+}
+
+// mujoco.mj_step for one env. Fin: ctrl in float64 (may be NaN / out of range; MuJoCo semantics).
+// CHECKS = false: mjx.step semantics (the brax kinds): no bad-state / bad-ctrl / bad-acc resets,
+// NaN propagates. F_NONNEG: see wrench_of.
+// (A speculative form -- step first, screen the loaded state afterwards -- measured slower.)
+template <typename T, bool CHECKS = true, bool F_NONNEG = false>
+QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[4]) {
+  // mj_checkPos / mj_checkVel: bad state => mj_resetData (qpos0, zero qvel, zero ctrl)
+  const bool bad = CHECKS ? check_state(e) : false;
+  // mj_fwdActuation: bad ctrl => all ctrl zeroed; ctrlrange clamp; site-transmission wrench
+  const bool zero = CHECKS && (bad || any_bad_ctrl<T>(Fin));
+  T qn[4] = {e.q[0], e.q[1], e.q[2], e.q[3]};
+  normalize4(qn);
+  ForceAcc<T> fa;
+  forward_base(c, qn, e.th, e.v, e.w, e.s, fa);
+  const Wrench<T> m = wrench_of<T, F_NONNEG>(c, Fin, zero);
+  physics_finish<T, CHECKS>(c, e, qn, fa, m);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -676,21 +721,30 @@ QD_HD bool terminated_of(const KConsts<T>& k, const float s12[12]) {
   return t;  // a NaN fails both compares; +-Inf is outside any finite bound
 }
 
-// (RateControlWrapper.action ->) HoverEnv.step for one env. The control path (CTBR, mixer,
-// voltage sag) runs in float64 like the reference; the rigid-body dynamics in T.
+// The control path of HoverEnv.step (float64 like the reference): RateControlWrapper.action
+// (CTBR: rate command -> torques, the float32 body rate of the last observation; the integral
+// state `rint` is updated), denormalize, _mix_to_motors, the voltage sag applied to the motor
+// commands, and the voltage update. Depends only on the action, the voltage (and, under CTBR, the
+// body rate and the integral) -- not on the rest of the state -- so k_step_h's helper waves run it
+// beside the step wave's physics. F[i] = clip(mix, 0, max) * vs >= 0 (or NaN).
+template <typename T>
+struct Ctl {
+  double F[4];  // motor commands (info["motor_commands"]), the ctrl handed to mj_step
+  double vs;    // info["voltage_scale"]
+  T volt;       // the updated voltage
+};
 template <typename T, bool CTBR>
-QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], StepRes& r,
-                    uint64_t* stamps = nullptr) {
+QD_HD Ctl<T> env_control(const KConsts<T>& k, T volt, const T w[3], T rint[3], const float act[4]) {
   float a[4];
   a[0] = act[0];
   if (CTBR) {
 #pragma unroll
     for (int j = 0; j < 3; j++) {
       const double des = double(act[1 + j]) * k.rate_max;
-      const double err = des - double(float(e.w[j]));  // _state.angular_velocity is float32
+      const double err = des - double(float(w[j]));  // _state.angular_velocity is float32
       const double taup = k.rate_ikd[j] * err;
-      const double ri = clipn(double(e.rint[j]) + k.rate_kidt * err, -k.rate_imax, k.rate_imax);
-      e.rint[j] = T(ri);
+      const double ri = clipn(double(rint[j]) + k.rate_kidt * err, -k.rate_imax, k.rate_imax);
+      rint[j] = T(ri);
       const double tau = taup + ri;
       a[1 + j] = float(clipn(tau * k.r_max_torque, -1.0, 1.0));
     }
@@ -700,35 +754,30 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
   double phys[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) phys[j] = double(denorm1(a[j], k.act_lo[j], k.act_span[j]));
-  double F[4];
+  Ctl<T> c;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double s = k.ph.mix[4 * i] * phys[0] + k.ph.mix[4 * i + 1] * phys[1] +
                      k.ph.mix[4 * i + 2] * phys[2] + k.ph.mix[4 * i + 3] * phys[3];
-    F[i] = clipn(s, 0.0, k.max_thrust);
+    c.F[i] = clipn(s, 0.0, k.max_thrust);
   }
-  const double vs = clipn(double(e.volt) * k.r_vnom, 0.0, 1.0);
-#pragma unroll
+  c.vs = clipn(double(volt) * k.r_vnom, 0.0, 1.0);
   // hover_env.py:175 clips F * vs to [0, max_thrust * vs]; that clip never binds here: F is in
   // [0, max_thrust] (or NaN) after the clip above, vs in [0, 1] (or NaN), max_thrust >= 0 (checked
   // by quad_create), and a rounded product with the same non-negative vs is monotone in F
   // (F * vs <= max_thrust * vs); NaN passes either way.
-  for (int i = 0; i < 4; i++) F[i] = F[i] * vs;
-  const double load = ((F[0] + F[1] + F[2] + F[3]) * 0.25) * k.r_mx;
+#pragma unroll
+  for (int i = 0; i < 4; i++) c.F[i] = c.F[i] * c.vs;
+  const double load = ((c.F[0] + c.F[1] + c.F[2] + c.F[3]) * 0.25) * k.r_mx;
   const double dV = (k.vb + k.vl * load) * k.dt;
-  e.volt = T(clipn(double(e.volt) - dV, k.vmin, k.vnom));
-  if (stamps) { QD_PIN_N(F, 4); QD_PIN(e.volt); }
-  QD_STAMP(stamps, 2);
-  // QD_ABL_*: cost-ablation builds of tools/step_variants.py only (never defined in the product)
-#if defined(QD_ABL_PHYS2)
-  physics_step<T, true, true>(k.ph, e, F);
-  physics_step<T, true, true>(k.ph, e, F);
-#elif !defined(QD_ABL_NOPHYS)
-  physics_step<T, true, true>(k.ph, e, F);  // F = clip(., 0, max) * vs >= 0 (or NaN)
-#endif
+  c.volt = T(clipn(double(volt) - dV, k.vmin, k.vnom));
+  return c;
+}
+
+// After mj_step: step count, QuadState + observation, reward, termination, truncation.
+template <typename T>
+QD_HD void env_post(const KConsts<T>& k, EnvRegs<T>& e, StepRes& r) {
   e.step += 1;
-  if (stamps) { QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.th, 4); QD_PIN_N(e.v, 3); QD_PIN_N(e.w, 3); QD_PIN_N(e.s, 4); }
-  QD_STAMP(stamps, 3);
 #if defined(QD_ABL_NOOBS)
 #pragma unroll
   for (int i = 0; i < 3; i++) {
@@ -740,14 +789,35 @@ QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], Step
 #else
   observe(k, e, r.obs, r.state12);
 #endif
-  if (stamps) { QD_PIN_N(r.obs, 12); QD_PIN_N(r.state12, 12); }
-  QD_STAMP(stamps, 4);
   r.reward = reward_of<T>(r.state12, e.target);
   r.term = terminated_of(k, r.state12);
   r.trunc = e.step >= k.max_steps;
+}
+
+// (RateControlWrapper.action ->) HoverEnv.step for one env: env_control, mujoco.mj_step
+// (physics_step, the rigid-body dynamics in T), env_post.
+template <typename T, bool CTBR>
+QD_HD void env_step(const KConsts<T>& k, EnvRegs<T>& e, const float act[4], StepRes& r,
+                    uint64_t* stamps = nullptr) {
+  const Ctl<T> c = env_control<T, CTBR>(k, e.volt, e.w, e.rint, act);
+  e.volt = c.volt;
+  if (stamps) { QD_PIN_N(c.F, 4); QD_PIN(e.volt); }
+  QD_STAMP(stamps, 2);
+  // QD_ABL_*: cost-ablation builds of tools/step_variants.py only (never defined in the product)
+#if defined(QD_ABL_PHYS2)
+  physics_step<T, true, true>(k.ph, e, c.F);
+  physics_step<T, true, true>(k.ph, e, c.F);
+#elif !defined(QD_ABL_NOPHYS)
+  physics_step<T, true, true>(k.ph, e, c.F);  // F = clip(., 0, max) * vs >= 0 (or NaN)
+#endif
+  if (stamps) { QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.th, 4); QD_PIN_N(e.v, 3); QD_PIN_N(e.w, 3); QD_PIN_N(e.s, 4); }
+  QD_STAMP(stamps, 3);
+  env_post(k, e, r);
+  if (stamps) { QD_PIN_N(r.obs, 12); QD_PIN_N(r.state12, 12); }
+  QD_STAMP(stamps, 4);
 #pragma unroll
-  for (int i = 0; i < 4; i++) r.motor[i] = float(F[i]);
-  r.vscale = float(vs);
+  for (int i = 0; i < 4; i++) r.motor[i] = float(c.F[i]);
+  r.vscale = float(c.vs);
   if (stamps) { QD_PIN(r.reward); QD_PIN(uint32_t(r.term)); QD_PIN(uint32_t(r.trunc)); QD_PIN_N(r.motor, 4); }
 }
 

@@ -278,22 +278,29 @@ __device__ __forceinline__ void step_body(const KConsts<float>& K, KParams p, co
 
 // ---------------------------------------------------------------------------------------------
 // k_step_h<KIND, CTBR, SPEC>: the step with HELPER waves. A block of 2 x HB threads owns HB envs:
-// the first HB/64 waves step one env per lane exactly as k_step; as many helper waves --
-// meanwhile draw every env's NEXT reset (the Philox words of its episode counter, the affine map,
-// the quaternion, the reset observation: reset_block / reset_affine_u / env_reset_from, the same
-// functions, so the same bits) into an LDS image, and after the block barrier a resetting step lane
-// only copies its row. The draw had been on the lone step wave's path (0.72 us of a 6.5 us step at
-// 65,536 envs, ablation build); the helpers run it in the issue slots the stalled step wave leaves.
-// HB = envs per block (one step wave + its helper wave per 64). Small batches take 64: at 4,096
-// envs 3.79 vs 4.24 us per launch with 256 (the batch spreads over 64 CUs instead of 16, and each
-// barrier joins two waves instead of eight); at 65,536 the two measured equal (5.84-5.87 vs
-// 5.83-5.87 us) and 128 slower (6.10), so batches above H_SMALL keep 256
-// (profiles/r02/ab_step_h_block.txt).
+// the first HB/64 waves step one env per lane; as many helper waves (one per SIMD, beside a step
+// wave) take the two parts of HoverEnv.step that do not depend on the rigid-body state:
+//   (C) the control path -- env_control: CTBR, denormalize, mixer, voltage sag, voltage update --
+//       and its motor wrench (wrench_of), handed to the step wave through LDS, plus the
+//       motor_commands / voltage_scale outputs. Meanwhile the step wave checks the state
+//       (mj_checkPos/Vel) and accumulates gravity, base drag and prop drags (forward_base), which
+//       need no controls; after barrier (C) it adds the wrench and finishes mj_step. Same
+//       functions in the same order as env_step, so the same bits as the one-wave forms.
+//   (R) every env's NEXT reset (the Philox words of its episode counter, the affine map, the
+//       quaternion, the reset observation: reset_block / reset_affine_u / env_reset_from) into an
+//       LDS image; after barrier (1) a resetting step lane only copies its row.
+// With one step wave per SIMD (65,536 envs) the step wave's chain is the launch: the helpers run
+// in the issue slots it leaves. HB = envs per block (one step wave + its helper wave per 64).
+// Small batches take 64: at 4,096 envs 3.79 vs 4.24 us per launch with 256 (the batch spreads over
+// 64 CUs instead of 16, and each barrier joins two waves instead of eight); at 65,536 the two
+// measured equal (5.84-5.87 vs 5.83-5.87 us) and 128 slower (6.10), so batches above H_SMALL keep
+// 256 (profiles/r02/ab_step_h_block.txt).
 constexpr int H_SMALL = 32768;
 constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
+constexpr int HCTL = 9;   // floats per env from the control helper: Fsum, taum 3, volt, bad ctrl, rint 3
 template <int KIND, bool CTBR, int HB>
 __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, const float4* __restrict__ act,
-                                            QuadStepOut out, float4* lds, float* H) {
+                                            QuadStepOut out, float4* lds, float* H, float* CT) {
   const int tid = threadIdx.x;
   const int block_first = p.first + blockIdx.x * HB;
   const int end = p.first + p.count;
@@ -302,15 +309,49 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
   const int i = live ? block_first + l : end - 1;
   const Tiles S(p);
   const uint32_t vo = env_off(uint32_t(i));
-  if (tid >= HB) {  // ---- helper: env i's next reset, into H[f][l]
+  if (tid >= HB) {  // ---- helper
+    // the helpers are the younger half of the block, the issue arbitration's losers: raised
+    // priority while their control path is on the step wave's path (to barrier C), then back
+    // (65,536 envs: 5.92 us vs 6.58 without; priority for the whole helper: 6.62 us)
+    __builtin_amdgcn_s_setprio(1);
+    // (C) env i's control path and motor wrench
     const uint32_t ep = S.ldu(F_EP, vo);
+    const float4 a4 = act[i];
+    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+    const float volt = S.ld(F_VOLT, vo);
+    float w[3] = {0.f, 0.f, 0.f}, ri[3] = {0.f, 0.f, 0.f};
+    if (CTBR) {
+#pragma unroll
+      for (int j = 0; j < 3; j++) { w[j] = S.ld(F_QVEL + 3 + j, vo); ri[j] = S.ld(F_RINT + j, vo); }
+    }
+    const Ctl<float> c = env_control<float, CTBR>(K, volt, w, ri, a);
+    const Wrench<float> m = wrench_of<float, true>(K.ph, c.F, false);  // F = clip(., 0, max) * vs >= 0
+    CT[0 * HB + l] = m.Fsum;
+#pragma unroll
+    for (int j = 0; j < 3; j++) CT[(1 + j) * HB + l] = m.taum[j];
+    CT[4 * HB + l] = c.volt;
+    CT[5 * HB + l] = any_bad_ctrl<float>(c.F) ? 1.f : 0.f;
+    if (CTBR) {
+#pragma unroll
+      for (int j = 0; j < 3; j++) CT[(6 + j) * HB + l] = ri[j];
+    }
+    if (live) {
+      const uint32_t o = uint32_t(i) * 4u;
+      if (out.motor_commands)
+        sto(reinterpret_cast<float4*>(out.motor_commands), 4u * o,
+            make_float4(float(c.F[0]), float(c.F[1]), float(c.F[2]), float(c.F[3])));
+      if (out.voltage_scale) sto(out.voltage_scale, o, float(c.vs));
+    }
+    __syncthreads();  // (C) the control results are staged
+    __builtin_amdgcn_s_setprio(0);
+    // (R) env i's next reset, into H[f][l]
     float u16[16];
 #pragma unroll
     for (uint32_t b = 0; b < 4; b++) {
-      uint32_t c[4];
-      reset_block(p.seed, p.gid_base + uint64_t(i), ep, b, c);
+      uint32_t cw[4];
+      reset_block(p.seed, p.gid_base + uint64_t(i), ep, b, cw);
 #pragma unroll
-      for (int j = 0; j < 4; j++) u16[4 * b + j] = u01(c[j]);
+      for (int j = 0; j < 4; j++) u16[4 * b + j] = u01(cw[j]);
     }
     float init12[12], tgt[3], obs[12], s12[12];
     reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
@@ -328,22 +369,49 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
   } else {  // ---- step
     float obs[12];
     EnvRegs<float> e;
+#if defined(QD_H_NOCTL)  // A/B builds only: the step wave runs the control path itself (round 2)
     load_env(p, i, e, CTBR);
     const uint32_t ep = S.ldu(F_EP, vo);
     const float4 a4 = act[i];
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
     StepRes r;
     env_step<float, CTBR>(K, e, a, r);
+    __syncthreads();  // (C)
+#else
+    load_env_motion(p, i, e);
+    const uint32_t ep = S.ldu(F_EP, vo);
+    // mujoco.mj_step up to the controls: mj_checkPos/Vel, gravity + base + prop drag
+    const bool bad = check_state(e);
+    float qn[4] = {e.q[0], e.q[1], e.q[2], e.q[3]};
+    normalize4(qn);
+    ForceAcc<float> fa;
+    forward_base(K.ph, qn, e.th, e.v, e.w, e.s, fa);
+    __syncthreads();  // (C)
+    Wrench<float> m;
+    m.Fsum = CT[0 * HB + l];
+#pragma unroll
+    for (int j = 0; j < 3; j++) m.taum[j] = CT[(1 + j) * HB + l];
+    e.volt = CT[4 * HB + l];
+    if (CTBR) {
+#pragma unroll
+      for (int j = 0; j < 3; j++) e.rint[j] = CT[(6 + j) * HB + l];
+    } else {
+      e.rint[0] = e.rint[1] = e.rint[2] = 0.f;
+    }
+    if (bad || CT[5 * HB + l] != 0.f) {  // mj_fwdActuation: bad state / bad ctrl -> zero ctrl
+      const double z[4] = {0.0, 0.0, 0.0, 0.0};
+      m = wrench_of<float, true>(K.ph, z, true);
+    }
+    physics_finish<float, true>(K.ph, e, qn, fa, m);
+    StepRes r;
+    env_post(K, e, r);
+#endif
     settle(ep);
     const uint32_t o = uint32_t(i) * 4u;
     if (live) {
       sto(out.reward, o, r.reward);
       sto(out.terminated, uint32_t(i), uint8_t(r.term));
       sto(out.truncated, uint32_t(i), uint8_t(r.trunc));
-      if (out.motor_commands)
-        sto(reinterpret_cast<float4*>(out.motor_commands), 4u * o,
-            make_float4(r.motor[0], r.motor[1], r.motor[2], r.motor[3]));
-      if (out.voltage_scale) sto(out.voltage_scale, o, r.vscale);
       if (out.state12) store_row12(out.state12, uint32_t(i), r.state12);
       if (out.target_info) {
         float info[9];
@@ -393,11 +461,12 @@ __global__ __launch_bounds__(2 * HB) void k_step_h(float* tiles, const float4* _
   p.kc = kc;
   __shared__ float4 lds[HB * 3];
   __shared__ float H[HROW * HB];
+  __shared__ float CT[(CTBR ? HCTL : HCTL - 3) * HB];
   if constexpr (SPEC) {
     constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
-    step_h_body<KIND, CTBR, HB>(K, p, act, out, lds, H);
+    step_h_body<KIND, CTBR, HB>(K, p, act, out, lds, H, CT);
   } else {
-    step_h_body<KIND, CTBR, HB>(*kc, p, act, out, lds, H);
+    step_h_body<KIND, CTBR, HB>(*kc, p, act, out, lds, H, CT);
   }
 }
 
@@ -1138,8 +1207,14 @@ __device__ __forceinline__ void step_g_body(const KConsts<float>& k, KParams p, 
   }
 }
 
+// QD_G_WAVES (A/B builds of tools/probe/build_variant.sh only): a minimum waves-per-SIMD target
+#if defined(QD_G_WAVES)
+#define QD_G_ATTR __attribute__((amdgpu_waves_per_eu(QD_G_WAVES, 8)))
+#else
+#define QD_G_ATTR
+#endif
 template <int KIND, bool CTBR, int G, bool SPEC>
-__global__ __launch_bounds__(BLOCK) void k_step_g(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
+__global__ __launch_bounds__(BLOCK) QD_G_ATTR void k_step_g(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
                                                   int32_t first, int32_t count, const KConsts<float>* __restrict__ kc,
                                                   KParams p, QuadStepOut out) {
   p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
