@@ -128,3 +128,33 @@ def test_relpos_over_rate_control_stack():
     w.close(); d.close()
     with pytest.raises(TypeError):
         RateControlWrapper(RelPosActWrapper(HoverEnv(device="cuda:0")))
+
+
+@pytest.mark.parametrize("one_launch", [True, False])
+def test_resume_draws_fresh_noise(one_launch):
+    """PPO.state_dict / load_state_dict (train.py --resume): a resumed run's rollouts draw the
+    action noise that follows the checkpoint, not the original run's from step 0 -- on the one-launch
+    path (quad_rollout, keyed by the host step counter) and the two-launch path (policy kernel +
+    env step, keyed by the device cursor, which graph capture zeroes)."""
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
+    cfg = PPOConfig(n_steps=16, n_minibatches=2, n_epochs=1, fused_rollout=one_launch)
+
+    def run(sd=None, rollouts=1):
+        env = QuadVecEnv(512, env="hover", device="cuda:0", seed=9)
+        algo = PPO(env, cfg, seed=2)
+        assert algo._one_launch == one_launch
+        if sd is not None:
+            algo.load_state_dict(sd)
+        acts = []
+        for _ in range(rollouts):
+            algo.collect_rollouts()
+            acts.append(algo.buf_act.clone())
+        out = algo.state_dict(), acts
+        env.close()
+        return out
+
+    sd, (a_first, a_second) = run(rollouts=2)
+    assert sd["noise_step"] == 2 * 16
+    _, (b_first,) = run(sd)  # same params, same env seed: only the noise can differ
+    assert not torch.equal(b_first, a_first)  # not a replay of the original run's first rollout

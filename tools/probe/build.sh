@@ -9,4 +9,4 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract
 O=../_lib/obj
 /opt/rocm/bin/hipcc $F -I$O -DQD_PROBE ${EXTRA:-} -c -o ../../tools/_build/obj/quadenv_probe.o quadenv.hip
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_build/probe.so \
-  ../../tools/_build/obj/quadenv_probe.o $O/policy.o $O/rollout.o $O/learner.o
+  ../../tools/_build/obj/quadenv_probe.o $O/policy.o $O/rollout.o $O/learner.o $O/learner_x3.o

@@ -309,6 +309,16 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
   const int i = live ? block_first + l : end - 1;
   const Tiles S(p);
   const uint32_t vo = env_off(uint32_t(i));
+#if defined(QD_PROBE)  // tools/probe/probe_step_h.py: per-wave stamps into the target_info buffer
+  uint64_t stamp_buf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t* stamps = out.target_info ? stamp_buf : nullptr;
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+  float* const stamp_out = out.target_info;
+  out.target_info = nullptr;
+#else
+  uint64_t* stamps = nullptr;
+#endif
+  QD_STAMP(stamps, 0);
   if (tid >= HB) {  // ---- helper
     // the helpers are the younger half of the block, the issue arbitration's losers: raised
     // priority while their control path is on the step wave's path (to barrier C), then back
@@ -324,6 +334,8 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #pragma unroll
       for (int j = 0; j < 3; j++) { w[j] = S.ld(F_QVEL + 3 + j, vo); ri[j] = S.ld(F_RINT + j, vo); }
     }
+    if (stamps) { QD_PIN(ep); QD_PIN(a4.x); QD_PIN(a4.w); QD_PIN(volt); }
+    QD_STAMP(stamps, 1);
     const Ctl<float> c = env_control<float, CTBR>(K, volt, w, ri, a);
     const Wrench<float> m = wrench_of<float, true>(K.ph, c.F, false);  // F = clip(., 0, max) * vs >= 0
     CT[0 * HB + l] = m.Fsum;
@@ -335,6 +347,8 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #pragma unroll
       for (int j = 0; j < 3; j++) CT[(6 + j) * HB + l] = ri[j];
     }
+    if (stamps) { QD_PIN(m.Fsum); QD_PIN(m.taum[0]); QD_PIN(m.taum[1]); QD_PIN(m.taum[2]); QD_PIN(c.volt); }
+    QD_STAMP(stamps, 2);
     if (live) {
       const uint32_t o = uint32_t(i) * 4u;
       if (out.motor_commands)
@@ -343,6 +357,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
       if (out.voltage_scale) sto(out.voltage_scale, o, float(c.vs));
     }
     __syncthreads();  // (C) the control results are staged
+    QD_STAMP(stamps, 3);
     __builtin_amdgcn_s_setprio(0);
     // (R) env i's next reset, into H[f][l]
     float u16[16];
@@ -364,8 +379,11 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
                              obs[10], obs[11]};
 #pragma unroll
     for (int f = 0; f < HROW; f++) H[f * HB + l] = row[f];
+    QD_STAMP(stamps, 4);
     __syncthreads();  // (1) the image is complete
+    QD_STAMP(stamps, 5);
     __syncthreads();  // (2) the obs rows are staged
+    QD_STAMP(stamps, 6);
   } else {  // ---- step
     float obs[12];
     EnvRegs<float> e;
@@ -380,13 +398,19 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #else
     load_env_motion(p, i, e);
     const uint32_t ep = S.ldu(F_EP, vo);
+    if (stamps) { QD_PIN(ep); QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.th, 4); QD_PIN_N(e.v, 3);
+                  QD_PIN_N(e.w, 3); QD_PIN_N(e.s, 4); QD_PIN_N(e.target, 3); QD_PIN(e.step); }
+    QD_STAMP(stamps, 1);
     // mujoco.mj_step up to the controls: mj_checkPos/Vel, gravity + base + prop drag
     const bool bad = check_state(e);
     float qn[4] = {e.q[0], e.q[1], e.q[2], e.q[3]};
     normalize4(qn);
     ForceAcc<float> fa;
     forward_base(K.ph, qn, e.th, e.v, e.w, e.s, fa);
+    if (stamps) { QD_PIN_N(fa.FB, 3); QD_PIN_N(fa.tau, 3); QD_PIN_N(fa.Qs, 4); QD_PIN_N(fa.R, 9); }
+    QD_STAMP(stamps, 2);
     __syncthreads();  // (C)
+    QD_STAMP(stamps, 3);
     Wrench<float> m;
     m.Fsum = CT[0 * HB + l];
 #pragma unroll
@@ -403,9 +427,13 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
       m = wrench_of<float, true>(K.ph, z, true);
     }
     physics_finish<float, true>(K.ph, e, qn, fa, m);
+    if (stamps) { QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.v, 3); QD_PIN_N(e.w, 3); }
+    QD_STAMP(stamps, 4);
     StepRes r;
     env_post(K, e, r);
 #endif
+    if (stamps) { QD_PIN_N(r.obs, 12); QD_PIN(r.reward); QD_PIN(uint32_t(r.term)); }
+    QD_STAMP(stamps, 5);
     settle(ep);
     const uint32_t o = uint32_t(i) * 4u;
     if (live) {
@@ -422,7 +450,9 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #pragma unroll
     for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
     const bool rs = live && (r.term || r.trunc) && p.auto_reset;
+    QD_STAMP(stamps, 6);
     __syncthreads();  // (1)
+    QD_STAMP(stamps, 7);
     if (rs) {
       if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
       float row[HROW];
@@ -445,12 +475,26 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     lds[3 * l + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
     lds[3 * l + 1] = make_float4(obs[4], obs[5], obs[6], obs[7]);
     lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
+    QD_STAMP(stamps, 8);
     __syncthreads();  // (2)
+    QD_STAMP(stamps, 9);
   }
   // the block's [HB,12] obs rows as contiguous float4 stores, shared by all 2 x HB threads
   const int nf4 = min(HB, end - block_first) * 3;
   float4* dst = reinterpret_cast<float4*>(out.obs + size_t(block_first) * 12);
   for (int idx = tid; idx < nf4; idx += 2 * HB) dst[idx] = lds[idx];
+#if defined(QD_PROBE)
+  QD_STAMP(stamps, 10);
+  if (stamps && (tid & 63) == 0) {  // wave (block, w): 16 words
+    uint64_t* st = reinterpret_cast<uint64_t*>(stamp_out) + (size_t(blockIdx.x) * (2 * HB / 64) + size_t(tid >> 6)) * 16;
+#pragma unroll
+    for (int k = 0; k < 11; k++) st[k] = stamp_buf[k];
+    st[12] = rt0;
+    st[13] = __builtin_amdgcn_s_memrealtime();
+    st[14] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+    st[15] = tid >= HB ? 1u : 0u;
+  }
+#endif
 }
 
 template <int KIND, bool CTBR, bool SPEC, int HB>

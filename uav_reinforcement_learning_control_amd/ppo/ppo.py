@@ -208,6 +208,7 @@ class PPO:
                          if self.cfg.fused_update and fusable and self.device.type == "cuda" else None)
         self._adam = FusedAdam(self.opt, self.cfg.max_grad_norm) if self._learner is not None else None
         self._t_host = 0  # running step counter of the one-launch path (keys the action noise)
+        self._cursor_resume = None  # the two-launch path's noise counter after load_state_dict
         self._noise_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5851F42D4C957F2D) & (2**64 - 1)
 
     # ------------------------------------------------------------------------------------
@@ -285,6 +286,9 @@ class PPO:
             self._started = True
             if use_graph and not self._one_launch:
                 self._capture()
+            if self._cursor_resume is not None:  # (after _capture's zeroing) resume the noise counter
+                self._cursor[0] = self._cursor_resume
+                self._cursor_resume = None
         if self._one_launch:
             return self._collect_one_launch()
         t0 = time.perf_counter()
@@ -432,8 +436,9 @@ class PPO:
     def state_dict(self) -> dict:
         """What a resumed run needs: policy, optimizer (Adam moments, step counts), the timestep
         count and the rollout's action-noise counter (so resumed rollouts draw fresh noise)."""
+        noise = self._t_host if self._one_launch else int(self._cursor[0].item())
         return {"policy": self.policy.state_dict(), "optimizer": self.opt.state_dict(),
-                "num_timesteps": self.num_timesteps, "noise_step": self._t_host}
+                "num_timesteps": self.num_timesteps, "noise_step": noise}
 
     def load_state_dict(self, sd: dict) -> None:
         """Restore state_dict() (parameters are copied in place, so the gradient bucket binding
@@ -445,5 +450,10 @@ class PPO:
             if "step" in st and torch.is_tensor(st["step"]):
                 st["step"] = st["step"].to(device=self.device, dtype=torch.float32)
         self.num_timesteps = int(sd["num_timesteps"])
-        self._t_host = int(sd.get("noise_step", 0))
+        ns = int(sd.get("noise_step", 0))
+        self._t_host = ns
+        # the two-launch path keys its noise on the device cursor, whose step count also selects the
+        # buffer row (t % n_steps): resume at the next rollout boundary
+        T = self.cfg.n_steps
+        self._cursor_resume = ((ns + T - 1) // T) * T
         self._started = False
