@@ -3,7 +3,7 @@
 // MFMA kernels for gfx950, with the per-step rollout epilogue fused in.
 //
 // Layout trick: every hidden layer is computed TRANSPOSED, H^T = W . X^T, with
-// v_mfma_f32_32x32x2_f32 (A = weights, B = activations). A 32x32 accumulator tile then holds
+// bf16 MFMA over three-piece splits (A = weights, B = activations; policy_net.h). A 32x32 accumulator tile then holds
 // neurons in its registers and envs on its lanes (col = lane & 31, row = (r & 3) + 8 (r >> 2) +
 // 4 (lane >> 5)), which is exactly the B-operand layout of the next layer if k-step r of that layer
 // consumes the input neurons held in register r -- so the whole MLP stays in registers. The
@@ -42,17 +42,18 @@ struct NetPtrs {
 };
 
 __device__ float pack_one(const NetPtrs& p, int nout, int idx) {
-  if (idx < NET_W2) {  // A[i = lane&31][k = lane>>5] of tile n, k-step s
-    const int s = idx % 8, lane = (idx / 8) % 64, n = idx / 512;
-    return s < 6 ? p.w0[(32 * n + (lane & 31)) * OBS + 2 * s + (lane >> 5)] : 0.f;
+  if (idx < NET_W2) {  // A[neuron 32n + lane&31][feature 8 (lane>>5) + j] of block n
+    const int j = idx % 8, lane = (idx / 8) % 64, n = idx / 512;
+    const int f = 8 * (lane >> 5) + j;
+    return f < OBS ? p.w0[(32 * n + (lane & 31)) * OBS + f] : 0.f;
   }
   if (idx < NET_B1) {
     int t = idx - NET_W2;
-    const int r = t % 4; t /= 4;
+    const int j = t % 8; t /= 8;
     const int lane = t % 64; t /= 64;
-    const int q = t % 4; t /= 4;
+    const int half = t % 2; t /= 2;
     const int n = t % 4, m = t / 4;
-    const int in = 32 * n + acc_row(4 * q + r, lane >> 5);  // input neuron held in register 4q+r
+    const int in = 32 * n + acc_row(8 * half + j, lane >> 5);  // input neuron held in register 8 half + j
     return p.w1[(32 * m + (lane & 31)) * H + in];
   }
   if (idx < NET_W3) {
@@ -85,10 +86,11 @@ __global__ void k_policy_pack(NetPtrs actor, NetPtrs critic, const float* __rest
   out[idx] = v;
 }
 
-__device__ __forceinline__ void load_xb(const float* __restrict__ x, int env, bool ok, float xb[6]) {
+// the input fragment of one env: features 8 (lane>>5) .. + 7 (zero past feature 11)
+__device__ __forceinline__ void load_xb(const float* __restrict__ x, int env, bool ok, float xb[8]) {
   const int h = (threadIdx.x & 63) >> 5;
 #pragma unroll
-  for (int s = 0; s < 6; s++) xb[s] = ok ? x[size_t(env) * OBS + 2 * s + h] : 0.f;
+  for (int k = 0; k < 8; k++) xb[k] = ok && (h == 0 || k < 4) ? x[size_t(env) * OBS + 8 * h + k] : 0.f;
 }
 
 
@@ -108,7 +110,7 @@ struct EpiArgs {  // QuadRolloutPost, flattened
 
 // Everything a tile reads from HBM, loaded in one go (issued a tile ahead, see k_policy_act).
 struct TileIn {
-  float xb[6];           // X^T fragments of the obs rows
+  float xb[8];           // X^T fragments of the obs rows
   float rew, ret, len;   // epilogue inputs (step t-1)
   uint32_t flags;        // bit0 terminated, bit1 truncated
 };
@@ -136,7 +138,7 @@ __device__ __forceinline__ float epilogue_tile(const float* __restrict__ Lc, con
   const bool timeout = ok && trunc && !term;
   float tv = 0.f;
   if (__any(timeout)) {
-    float xb[1][6], v[1][1];
+    float xb[1][8], v[1][1];
     load_xb(e.terminal_obs, env, ok, xb[0]);
     net_forward<1, 1>(Lc, xb, v);
     tv = v[0][0];
@@ -242,7 +244,7 @@ __global__ __launch_bounds__(BLK) void k_policy_act(const float* __restrict__ pa
     }
     int envs[NT_ACT];
     bool oks[NT_ACT];
-    float ls[NT_ACT], xb[NT_ACT][6];
+    float ls[NT_ACT], xb[NT_ACT][8];
 #pragma unroll
     for (int j = 0; j < NT_ACT; j++) {
       envs[j] = (g * NT_ACT + j) * TILE + (lane & 31);
@@ -251,7 +253,7 @@ __global__ __launch_bounds__(BLK) void k_policy_act(const float* __restrict__ pa
       if (pend) ls[j] = epilogue_tile(lds + ACTOR_F, e, cur[j], envs[j], oks[j], rowp, st);
       else if (a.last_start && oks[j]) ls[j] = a.last_start[envs[j]];
 #pragma unroll
-      for (int s = 0; s < 6; s++) xb[j][s] = cur[j].xb[s];
+      for (int k = 0; k < 8; k++) xb[j][k] = cur[j].xb[k];
     }
     float mean[NT_ACT][ACT], val[NT_ACT][1];
     net_forward<ACT, NT_ACT>(lds, xb, mean);
@@ -263,7 +265,8 @@ __global__ __launch_bounds__(BLK) void k_policy_act(const float* __restrict__ pa
       if (!oks[j]) continue;
       if (a.obs_copy) {
 #pragma unroll
-        for (int s = 0; s < 6; s++) a.obs_copy[(row0 + env) * OBS + 2 * s + h] = xb[j][s];
+        for (int k = 0; k < 8; k++)
+          if (h == 0 || k < 4) a.obs_copy[(row0 + env) * OBS + 8 * h + k] = xb[j][k];
       }
       if (h) continue;  // one lane per env from here
       if (a.starts) a.starts[row0 + env] = ls[j];

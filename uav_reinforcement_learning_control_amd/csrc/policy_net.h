@@ -1,5 +1,14 @@
 // policy_net.h -- the rollout policy's MLP on MFMA (device only), shared by the policy kernel
 // (policy.hip) and the fused rollout kernel (rollout.hip). See policy.hip for the layout trick.
+//
+// Arithmetic: bf16 MFMA (v_mfma_f32_32x32x16_bf16) over three-piece splits of every f32 operand,
+// the learner's scheme (learner_x3.hip): x = x0 + x1 + x2, each piece the round-to-nearest bf16 of
+// what the previous pieces leave (exact), and a product a*b as the six MFMAs a2b0 + a1b1 + a0b2 +
+// a1b0 + a0b1 + a0b0 accumulated in f32; the dropped a1b2 + a2b1 + a2b2 are <= ~2^-23 |ab|. One
+// 16-deep k-step costs 6 x 32 matrix cycles instead of 8 x 64 with v_mfma_f32_32x32x2_f32 (2.7x
+// less). The activations (X^T, relu(h1)^T) are split once per layer; the weights are staged in LDS
+// as f32 (both nets' three-piece W2 would be 192 KB against 160) and split at use, each split
+// shared by the NT tiles of the wave.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -10,19 +19,25 @@
 namespace quadenv {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int H = 128, OBS = 12, ACT = 4;
 constexpr int TILE = 32;     // envs per MFMA tile (one wave holds one tile at a time)
 constexpr int PBLOCK = 256;  // 4 waves (k_rollout_post; k_policy_act takes BLK)
 
-// packed net image (floats); NOUT = 4 (actor) or 1 (critic):
-//   W1: [4 n][64 lane][8]              layer-1 A fragments, k-steps s = 0..5 (6, 7 zero)
-//   W2: [4 m][4 n][4 q][64 lane][4 r]   layer-2 A fragments, k-step 4q + r of input tile n
+// packed net image (floats); NOUT = 4 (actor) or 1 (critic). Operand element j of lane l (r = l & 31,
+// h = l >> 5) is k = 8h + j of the 32x32x16 MFMA (cdna_hip_programming.md, bf16 lane maps):
+//   W1: [4 n][64 lane][8]               A[neuron 32n + r][feature 8h + j] (features 12..15 zero)
+//   W2: [4 m][4 n][2 t][64 lane][8]     A[neuron 32m + r][input 32n + acc_row(8t + j, h)]: k-step
+//                                       (n, t) consumes registers 8t .. 8t + 7 of relu(h1) block n
 //   B1, B2: [4 tile][2 half][16 reg]    biases in accumulator order
 //   W3 actor:  [4 m][16 reg][2 half][4 out]   head weights in accumulator order
 //   W3 critic: [4 m][4 rq][2 half][4 r]       (reg = 4 rq + r)
 //   B3: [4]
-constexpr int W1_F = 4 * 64 * 8, W2_F = 4 * 4 * 4 * 64 * 4, B_F = 4 * 2 * 16;
+constexpr int W1_F = 4 * 64 * 8, W2_F = 4 * 4 * 2 * 64 * 8, B_F = 4 * 2 * 16;
 constexpr int NET_W1 = 0, NET_W2 = NET_W1 + W1_F, NET_B1 = NET_W2 + W2_F, NET_B2 = NET_B1 + B_F;
 constexpr int NET_W3 = NET_B2 + B_F;
 constexpr int ACTOR_F = NET_W3 + ACT * 128 + 4;
@@ -55,11 +70,12 @@ __device__ __forceinline__ void bias_init(f32x16& acc, const float* L, int off) 
 
 // 1/16 of one 32-neuron block's head: ReLU of accumulator register(s) `i` (actor: register i; critic:
 // registers 4(i/4).. handled at i % 4 == 0) times the packed head weights, into part[][].
+// (o3 = NET_W3 + 4h: the lane's part of the head-weight region)
 template <int NOUT, int NT>
 __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32x16 (&x)[NT], int m, int i,
-                                          int h, float (&part)[NT][NOUT]) {
+                                          int o3, float (&part)[NT][NOUT]) {
   if constexpr (NOUT == ACT) {
-    const float4 w = ld4(L, NET_W3 + ((m * 16 + i) * 2 + h) * 4);
+    const float4 w = ld4(L, o3 + (m * 16 + i) * 8);
 #pragma unroll
     for (int j = 0; j < NT; j++) {
       const float v = relu(x[j][i]);
@@ -70,7 +86,7 @@ __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32
     }
   } else {
     if (i % 4 != 0) return;
-    const float4 w = ld4(L, NET_W3 + ((m * 4 + i / 4) * 2 + h) * 4);
+    const float4 w = ld4(L, o3 + (m * 4 + i / 4) * 8);
 #pragma unroll
     for (int j = 0; j < NT; j++) {
       part[j][0] = fmaf(w.x, relu(x[j][i + 0]), part[j][0]);
@@ -81,33 +97,147 @@ __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32
   }
 }
 
-// ---- one net's forward for NT 32-env tiles at once (all 64 lanes). X^T fragments:
-// xb[j][s] = x[env = lane&31 of tile j][2 s + (lane>>5)]. Returns the NOUT head outputs of env
-// lane&31 of every tile (both lane halves get them). The NT tiles share every LDS weight fragment,
-// and their MFMA chains interleave, so consecutive MFMAs are independent.
+// ---- three-piece operands
+struct P3 {
+  bf16x8 p[3];  // x = p[0] + p[1] + p[2]
+};
+__device__ __forceinline__ P3 split8(const float (&v)[8]) {
+  u32x4 q0, q1, q2;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const f32x2 x = {v[2 * k], v[2 * k + 1]};
+    const bf16x2 p0 = __builtin_convertvector(x, bf16x2);
+    const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
+    const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
+    const f32x2 r2 = r1 - __builtin_convertvector(p1, f32x2);
+    const bf16x2 p2 = __builtin_convertvector(r2, bf16x2);
+    q0[k] = __builtin_bit_cast(uint32_t, p0);
+    q1[k] = __builtin_bit_cast(uint32_t, p1);
+    q2[k] = __builtin_bit_cast(uint32_t, p2);
+  }
+  P3 o;
+  o.p[0] = __builtin_bit_cast(bf16x8, q0);
+  o.p[1] = __builtin_bit_cast(bf16x8, q1);
+  o.p[2] = __builtin_bit_cast(bf16x8, q2);
+  return o;
+}
+// acc += a * b, small terms first
+__device__ __forceinline__ f32x16 mfma6(const P3& a, const P3& b, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[2], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[1], b.p[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[1], acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.p[0], b.p[0], acc, 0, 0, 0);
+}
+__device__ __forceinline__ P3 ld_split8(const float* L, int off) {
+  const float4 a = ld4(L, off), b = ld4(L, off + 4);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  return split8(v);
+}
+
+// ---- one net's forward for NT 32-env tiles at once (all 64 lanes). Input fragments:
+// xq[j][k] = x[env = lane&31 of tile j][feature 8 (lane>>5) + k] (zero past feature 11). Returns the
+// NOUT head outputs of env lane&31 of every tile (both lane halves get them). The NT tiles share
+// every weight split, and their MFMA chains interleave.
+// Order: per input block n, layer 1 makes relu(h1) block n as pieces, and its two k-steps go into
+// all four layer-2 output blocks (m) at once, so only two blocks of pieces are ever live (all four
+// would be 192 VGPRs at NT = 2); the layer-2 accumulators (128 registers) sit in AGPRs. Software
+// pipeline over the 32 layer-2 k-steps g = 8n + s (s = 4t + m): the W2 fragment of step g + 2 is
+// read from LDS and the one of g + 1 split while step g's 6 x NT MFMAs issue; during block n,
+// layer 1 of block n + 1 runs too (its W1 split at s = 0, its MFMAs at s = 1, its ReLU + split at
+// s = 3..6), so the matrix pipe never waits for a layer-1 result. Each step is one scheduling
+// region (fence) with its VALU interleaved between the MFMAs.
+template <int NT>
+__device__ __forceinline__ void relu_split(const f32x16& a, int t, P3& out) {
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = relu(a[8 * t + k]);
+  out = split8(v);
+}
+
 template <int NOUT, int NT>
-__device__ __forceinline__ void net_forward(const float* __restrict__ L, const float (&xb)[NT][6],
+__device__ __forceinline__ void net_forward(const float* __restrict__ L, const float (&xq)[NT][8],
                                             float (&out)[NT][NOUT]) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
-  f32x16 h1[NT][4];
+  // per-region lane offsets, opaque to the compiler: every read below is one of these plus an
+  // immediate (< 64 KB). Left to itself it hoists one address register per distinct offset out of
+  // the callers' step loops (the critic's image starts 76 KB into the LDS) -- ~100 of them, spilled.
+  int o1 = NET_W1 + lane * 8, o2 = NET_W2 + lane * 8, ob = NET_B1 + h * 16, o3 = NET_W3 + h * 4;
+  asm volatile("" : "+v"(o1), "+v"(o2), "+v"(ob), "+v"(o3));
+  P3 xp[NT];
 #pragma unroll
-  for (int n = 0; n < 4; n++) {
+  for (int j = 0; j < NT; j++) xp[j] = split8(xq[j]);
+  f32x16 acc[4][NT];
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    bias_init(acc[m][0], L, ob + B_F + m * 32);
+#pragma unroll
+    for (int j = 1; j < NT; j++) acc[m][j] = acc[m][0];
+  }
+  // W2 fragment of global k-step g = 8n + 4t + m
+  auto frag = [&](int g) { return o2 + (((g & 3) * 4 + (g >> 3)) * 2 + ((g >> 2) & 1)) * 512; };
+  P3 h1[2][NT][2];  // relu(h1) pieces of blocks n (buffer n & 1) and n + 1
+  {
     f32x16 b;
-    bias_init(b, L, NET_B1 + (n * 2 + h) * 16);
-    const float4 wa = ld4(L, NET_W1 + (n * 64 + lane) * 8), wb = ld4(L, NET_W1 + (n * 64 + lane) * 8 + 4);
-    const float w[6] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y};
-    f32x16 acc[NT];
-#pragma unroll
-    for (int j = 0; j < NT; j++) acc[j] = b;
-#pragma unroll
-    for (int s = 0; s < 6; s++)
-#pragma unroll
-      for (int j = 0; j < NT; j++) acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[s], xb[j][s], acc[j], 0, 0, 0);
+    bias_init(b, L, ob);
+    const P3 w1 = ld_split8(L, o1);
 #pragma unroll
     for (int j = 0; j < NT; j++) {
+      const f32x16 a1 = mfma6(w1, xp[j], b);
+      relu_split<NT>(a1, 0, h1[0][j][0]);
+      relu_split<NT>(a1, 1, h1[0][j][1]);
+    }
+  }
+  float4 raw[2][2];  // W2 fragments read ahead (ring of two steps)
+  raw[0][0] = ld4(L, frag(0)); raw[0][1] = ld4(L, frag(0) + 4);
+  raw[1][0] = ld4(L, frag(1)); raw[1][1] = ld4(L, frag(1) + 4);
+  P3 w;
+  {
+    const float v[8] = {raw[0][0].x, raw[0][0].y, raw[0][0].z, raw[0][0].w,
+                        raw[0][1].x, raw[0][1].y, raw[0][1].z, raw[0][1].w};
+    w = split8(v);
+  }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int r = 0; r < 16; r++) acc[j][r] = relu(acc[j][r]);
-      h1[j][n] = acc[j];
+  for (int n = 0; n < 4; n++) {
+    const int cb = n & 1, nb = cb ^ 1;
+    P3 w1n;
+    f32x16 b1n, a1n[NT];
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+      const int g = 8 * n + s, t = s >> 2, m = s & 3;
+      if (g + 2 < 32) {  // read step g + 2's fragment into the slot step g's split just freed
+        raw[g & 1][0] = ld4(L, frag(g + 2));
+        raw[g & 1][1] = ld4(L, frag(g + 2) + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < NT; j++) acc[m][j] = mfma6(w, h1[cb][j][t], acc[m][j]);
+      if (n < 3 && s == 1) {
+#pragma unroll
+        for (int j = 0; j < NT; j++) a1n[j] = mfma6(w1n, xp[j], b1n);
+      }
+      P3 wn;
+      if (g + 1 < 32) {
+        const float4 r0 = raw[(g + 1) & 1][0], r1 = raw[(g + 1) & 1][1];
+        const float v[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        wn = split8(v);
+      }
+      if (n < 3 && s == 0) {
+        bias_init(b1n, L, ob + (n + 1) * 32);
+        w1n = ld_split8(L, o1 + (n + 1) * 512);
+      }
+      if (n < 3 && s >= 3 && s <= 6) {
+        const int u = s - 3;  // tile u >> 1, half u & 1 (NT = 1: halves at s = 3, 4)
+        if ((u >> 1) < NT) relu_split<NT>(a1n[u >> 1], u & 1, h1[nb][u >> 1][u & 1]);
+      }
+#pragma unroll
+      for (int q = 0; q < 6 * NT; q++) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (g + 1 < 32) w = wn;
     }
   }
   float part[NT][NOUT];
@@ -115,49 +245,19 @@ __device__ __forceinline__ void net_forward(const float* __restrict__ L, const f
   for (int j = 0; j < NT; j++)
 #pragma unroll
     for (int o = 0; o < NOUT; o++) part[j][o] = 0.f;
-  // Layer 2 in four 32-neuron blocks m. The VALU head of block m-1 is issued inside block m's MFMA
-  // chain (independent work), so it runs in the matrix pipe's shadow instead of after it.
-  f32x16 prev[NT];  // block m-1 (zeros before block 0: its head then adds exact zeros)
 #pragma unroll
-  for (int j = 0; j < NT; j++)
-#pragma unroll
-    for (int r = 0; r < 16; r++) prev[j][r] = 0.f;
-#pragma unroll 1
   for (int m = 0; m < 4; m++) {
-    f32x16 acc[NT];
-    bias_init(acc[0], L, NET_B2 + (m * 2 + h) * 16);
 #pragma unroll
-    for (int j = 1; j < NT; j++) acc[j] = acc[0];
-    // A fragments double-buffered: fragment i+1 is in flight while the MFMAs of fragment i issue
-    // (one register quad would make each ds_read wait for the last MFMA that reads it)
-    const int wbase = NET_W2 + (m * 16 * 64 + lane) * 4;
-    float4 a4 = ld4(L, wbase);
-#pragma unroll
-    for (int i = 0; i < 16; i++) {  // i = 4 n + q
-      const int n = i / 4, q = i % 4;
-      float4 nx;
-      if (i < 15) nx = ld4(L, wbase + (i + 1) * 64 * 4);
-      const float w[4] = {a4.x, a4.y, a4.z, a4.w};
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-#pragma unroll
-        for (int j = 0; j < NT; j++)
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[k], h1[j][n][4 * q + k], acc[j], 0, 0, 0);
-      head_part<NOUT, NT>(L, prev, m > 0 ? m - 1 : 0, i, h, part);  // 1/16 of block m-1's head
-      if (i < 15) a4 = nx;
-    }
-#pragma unroll
-    for (int j = 0; j < NT; j++) prev[j] = acc[j];
+    for (int i = 0; i < 16; i++) head_part<NOUT, NT>(L, acc[m], m, i, o3, part);
+    __builtin_amdgcn_sched_barrier(0);  // one block's accumulators in VGPRs at a time
   }
-#pragma unroll
-  for (int i = 0; i < 16; i++) head_part<NOUT, NT>(L, prev, 3, i, h, part);
   // lanes l and l ^ 32 hold the two halves of the same env's neurons; both lanes form the same sum
 #pragma unroll
   for (int j = 0; j < NT; j++)
 #pragma unroll
     for (int o = 0; o < NOUT; o++) {
       const float other = __shfl_xor(part[j][o], 32);
-      out[j][o] = ((h ? other : part[j][o]) + (h ? part[j][o] : other)) + L[NET_W3 + NOUT * 128 + o];
+      out[j][o] = ((h ? other : part[j][o]) + (h ? part[j][o] : other)) + L[o3 - 4 * h + NOUT * 128 + o];
     }
 }
 

@@ -40,19 +40,20 @@ namespace {
 constexpr int RBLOCK = 256;  // envs per block; one block per CU (the LDS holds the nets)
 constexpr int ROLLOUT_NT_DEFAULT = 2;
 
-// X^T fragments of the wave's tile(s) from the per-thread observation rows (see top).
+// X^T fragments of the wave's tile(s) from the per-thread observation rows (see top): lane half h
+// takes features 8h .. 8h + 7 (zero past feature 11) of its env in each tile.
 template <int NT>
-__device__ __forceinline__ void fragments(const float ob[12], float (&xb)[NT][6]) {
+__device__ __forceinline__ void fragments(const float ob[12], float (&xb)[NT][8]) {
   const bool h = (threadIdx.x & 32) != 0;
 #pragma unroll
-  for (int s = 0; s < 6; s++) {
-    const float lo = ob[2 * s], hi = ob[2 * s + 1];
+  for (int k = 0; k < 8; k++) {
+    const float lo = ob[k], hi = k < 4 ? ob[8 + k] : 0.f;  // this env's features k and 8 + k
     if constexpr (NT == 2) {  // lane l's env is tile (l >> 5)'s env l & 31
       const float got = __shfl_xor(h ? lo : hi, 32);
-      xb[0][s] = h ? got : lo;
-      xb[NT - 1][s] = h ? hi : got;
+      xb[0][k] = h ? got : lo;
+      xb[NT - 1][k] = h ? hi : got;
     } else {  // both lane halves carry env l & 31
-      xb[0][s] = h ? hi : lo;
+      xb[0][k] = h ? hi : lo;
     }
   }
 }
@@ -147,7 +148,7 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
     const uint32_t t = a.t0 + uint32_t(s);
     const size_t row = size_t(t % a.rows) * n + size_t(i);
     // ---- policy: both nets on the wave's two tiles, then this lane's env
-    float xb[NT][6], mean[NT][ACT], val[NT][1];
+    float xb[NT][8], mean[NT][ACT], val[NT][1];
     fragments<NT>(ob, xb);
     // QD_ROLL_*: cost-ablation builds of tools/rollout_variants.py only (never defined in the product)
 #if defined(QD_ROLL_NOMLP)
@@ -198,7 +199,7 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
     const bool timeout = ok && r.trunc && !r.term;
     float tv = 0.f;
     if (__any(timeout)) {
-      float xt[NT][6], vt[NT][1];
+      float xt[NT][8], vt[NT][1];
       fragments<NT>(r.obs, xt);
       net_forward<1, NT>(lds + ACTOR_F, xt, vt);
       tv = (NT == 2 && h) ? vt[NT - 1][0] : vt[0][0];
