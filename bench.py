@@ -348,10 +348,20 @@ def _rollout_phase(env, args) -> dict:
     graph-replayed) and the same step as torch ops on the same policy."""
     from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
     out = {"n_steps": args.rollout_steps,
-           "what": "actor+critic MLP 12-128-128 fp32 + Gaussian sample + clip + env step + "
+           "what": "actor+critic MLP 12-128-128 (f32-level, bf16x3 MFMA) + Gaussian sample + clip + env step + "
                    "TimeLimit bootstrap + buffer rows; GAE included"}
     n = env.num_envs
     flop_step = n * (2 * 2 * (12 * 128 + 128 * 128) + 2 * 128 * 5)  # both nets + heads, per env-step
+
+    def mlp_roofline(flop, us, steps):
+        # bf16 MFMA on three-piece splits (csrc/policy_net.h): per 64 envs (one wave, two 32-env
+        # tiles) and step, (4 layer-1 + 32 layer-2) k-steps x 6 v_mfma_f32_32x32x16_bf16 x 2 tiles
+        # x 2 nets = 864 MFMAs of 32 cycles on the wave's SIMD
+        floor_us = steps * 864 * 32 * (n / 64) / 1024 / 2.4e3  # 1,024 SIMDs at the 2.4 GHz peak clock
+        return {"f32_equivalent_TFLOPs": flop / (us * 1e-6) / 1e12, "peak_TFLOPs": 157.3,
+                "f32_equivalent_frac": flop / (us * 1e-6) / 1e12 / 157.3,
+                "matrix_pipe_floor_us": floor_us, "matrix_pipe_frac": floor_us / us,
+                "bound": "mfma (bf16 32x32x16 on three-piece splits: f32-level error)"}
     for name, fused, one in (("one_launch", True, True), ("mfma", True, False), ("torch", False, False)):
         m = PPO(env, PPOConfig(n_steps=args.rollout_steps, fused_policy=fused, fused_rollout=one), seed=0)
         m.collect_rollouts(use_graph=True)  # capture + warm
@@ -379,8 +389,7 @@ def _rollout_phase(env, args) -> dict:
                 "kernel": "k_rollout<HOVER,noCTBR>", "steps_per_launch": args.rollout_steps,
                 "kernel_us": us, "us_per_step": us / args.rollout_steps,
                 "env_steps_per_s": n * args.rollout_steps / (us * 1e-6),
-                "flop_per_launch": flop, "achieved_TFLOPs": flop / (us * 1e-6) / 1e12,
-                "peak_TFLOPs": 157.3, "bound": "mfma (fp32 32x32x2)"}
+                "flop_per_launch": flop, **mlp_roofline(flop, us, args.rollout_steps)}
         elif fused:  # the two-launch path's policy kernel alone: MFMA roofline
             ae = torch.empty(n, 4, device=env.device)
             for _ in range(5):
@@ -393,9 +402,7 @@ def _rollout_phase(env, args) -> dict:
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / 100
             out["policy_kernel"] = {"kernel": "k_policy_act<2,256>", "kernel_us": us,
-                                    "flop_per_launch": flop_step,
-                                    "achieved_TFLOPs": flop_step / (us * 1e-6) / 1e12,
-                                    "peak_TFLOPs": 157.3, "bound": "mfma (fp32 32x32x2)"}
+                                    "flop_per_launch": flop_step, **mlp_roofline(flop_step, us, 1)}
         del m
         torch.cuda.empty_cache()
     out["env_steps_per_s"] = out["one_launch"]["env_steps_per_s"]

@@ -25,8 +25,7 @@ __global__ __launch_bounds__(BLK) void k_nf(const float* __restrict__ packed, fl
   float accum = 0.f;
   for (int it = 0; it < iters; it++) {
     float mean[NT][4], val[NT][1];
-    net_forward<4, NT>(lds, xq, mean);
-    net_forward<1, NT>(lds + ACTOR_F, xq, val);
+    net_forward2<NT>(lds, xq, mean, val);
     for (int j = 0; j < NT; j++) {
       accum += mean[j][0] + mean[j][3] + val[j][0];
       xq[j][it & 7] += 1e-3f * mean[j][1];

@@ -256,8 +256,7 @@ __global__ __launch_bounds__(BLK) void k_policy_act(const float* __restrict__ pa
       for (int k = 0; k < 8; k++) xb[j][k] = cur[j].xb[k];
     }
     float mean[NT_ACT][ACT], val[NT_ACT][1];
-    net_forward<ACT, NT_ACT>(lds, xb, mean);
-    net_forward<1, NT_ACT>(lds + ACTOR_F, xb, val);
+    net_forward2<NT_ACT>(lds, xb, mean, val);
 #pragma unroll
     for (int j = 0; j < NT_ACT; j++) {
       const int env = envs[j];

@@ -136,8 +136,8 @@ __device__ __forceinline__ P3 ld_split8(const float* L, int off) {
   return split8(v);
 }
 
-// ---- one net's forward for NT 32-env tiles at once (all 64 lanes). Input fragments:
-// xq[j][k] = x[env = lane&31 of tile j][feature 8 (lane>>5) + k] (zero past feature 11). Returns the
+// ---- the MLP forward for NT 32-env tiles at once (all 64 lanes). Input fragments:
+// xq[j][k] = x[env = lane&31 of tile j][feature 8 (lane>>5) + k] (zero past feature 11). Outputs: the
 // NOUT head outputs of env lane&31 of every tile (both lane halves get them). The NT tiles share
 // every weight split, and their MFMA chains interleave.
 // Order: per input block n, layer 1 makes relu(h1) block n as pieces, and its two k-steps go into
@@ -145,120 +145,197 @@ __device__ __forceinline__ P3 ld_split8(const float* L, int off) {
 // would be 192 VGPRs at NT = 2); the layer-2 accumulators (128 registers) sit in AGPRs. Software
 // pipeline over the 32 layer-2 k-steps g = 8n + s (s = 4t + m): the W2 fragment of step g + 2 is
 // read from LDS and the one of g + 1 split while step g's 6 x NT MFMAs issue; during block n,
-// layer 1 of block n + 1 runs too (its W1 split at s = 0, its MFMAs at s = 1, its ReLU + split at
-// s = 3..6), so the matrix pipe never waits for a layer-1 result. Each step is one scheduling
-// region (fence) with its VALU interleaved between the MFMAs.
-template <int NT>
-__device__ __forceinline__ void relu_split(const f32x16& a, int t, P3& out) {
-  float v[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) v[k] = relu(a[8 * t + k]);
-  out = split8(v);
+// layer 1 of the NEXT block runs too (its W1 split at s = 0, its MFMAs at s = 1, its ReLU + split in
+// 16 pair-chunks over s = 2..7), so the matrix pipe never waits for a layer-1 result. When the
+// actor is followed by the critic (net_forward2), the critic's block 0 and first W2 fragments are
+// that next block: the pipeline runs through both nets. Each step is one scheduling region (fence)
+// with its VALU interleaved between the MFMAs.
+
+// per-net LDS offsets of this lane (floats), opaque to the compiler: every read is one of these
+// plus an immediate (< 64 KB). Left to itself it hoists one address register per distinct offset out
+// of the callers' step loops (the critic's image starts 76 KB into the LDS) -- ~100 of them, spilled.
+// VALU per MFMA in each step's interleave (A/B builds of tools/diag/net_bench.hip; 0: the scheduler's own order)
+#ifndef QD_NF_VPG
+#define QD_NF_VPG 5
+#endif
+struct NetOff {
+  int w1, w2, b, w3;
+};
+__device__ __forceinline__ NetOff net_off(int base) {
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  NetOff o{base + NET_W1 + lane * 8, base + NET_W2 + lane * 8, base + NET_B1 + h * 16, base + NET_W3 + h * 4};
+  asm volatile("" : "+v"(o.w1), "+v"(o.w2), "+v"(o.b), "+v"(o.w3));
+  return o;
+}
+// W2 fragment of layer-2 k-step g = 8n + 4t + m
+__device__ __forceinline__ int w2_frag(const NetOff& o, int g) {
+  return o.w2 + (((g & 3) * 4 + (g >> 3)) * 2 + ((g >> 2) & 1)) * 512;
 }
 
-template <int NOUT, int NT>
-__device__ __forceinline__ void net_forward(const float* __restrict__ L, const float (&xq)[NT][8],
-                                            float (&out)[NT][NOUT]) {
-  const int lane = threadIdx.x & 63, h = lane >> 5;
-  // per-region lane offsets, opaque to the compiler: every read below is one of these plus an
-  // immediate (< 64 KB). Left to itself it hoists one address register per distinct offset out of
-  // the callers' step loops (the critic's image starts 76 KB into the LDS) -- ~100 of them, spilled.
-  int o1 = NET_W1 + lane * 8, o2 = NET_W2 + lane * 8, ob = NET_B1 + h * 16, o3 = NET_W3 + h * 4;
-  asm volatile("" : "+v"(o1), "+v"(o2), "+v"(ob), "+v"(o3));
-  P3 xp[NT];
+struct Q3 {  // three pieces as raw 32-bit words (filled a pair at a time)
+  u32x4 q[3];
+  __device__ __forceinline__ P3 p() const {
+    P3 o;
 #pragma unroll
-  for (int j = 0; j < NT; j++) xp[j] = split8(xq[j]);
+    for (int k = 0; k < 3; k++) o.p[k] = __builtin_bit_cast(bf16x8, q[k]);
+    return o;
+  }
+};
+// pieces of the pair (x0, x1) into word `k` of each piece (one quarter of split8)
+__device__ __forceinline__ void split_pair(float x0, float x1, Q3& o, int k) {
+  const f32x2 x = {x0, x1};
+  const bf16x2 p0 = __builtin_convertvector(x, bf16x2);
+  const f32x2 r1 = x - __builtin_convertvector(p0, f32x2);
+  const bf16x2 p1 = __builtin_convertvector(r1, bf16x2);
+  const f32x2 r2 = r1 - __builtin_convertvector(p1, f32x2);
+  const bf16x2 p2 = __builtin_convertvector(r2, bf16x2);
+  o.q[0][k] = __builtin_bit_cast(uint32_t, p0);
+  o.q[1][k] = __builtin_bit_cast(uint32_t, p1);
+  o.q[2][k] = __builtin_bit_cast(uint32_t, p2);
+}
+
+template <int NT>
+struct Pipe {
+  Q3 h1[2][NT][2];   // relu(h1) pieces: block n in buffer n & 1 (block 0 of the next net: buffer 0)
+  float4 raw[2][2];  // W2 fragments read ahead (ring of two steps)
+  P3 w;              // the current step's W2 split
+};
+
+// block 0 of a net before its pipeline starts (the first net of a call)
+template <int NT>
+__device__ __forceinline__ void pipe_start(const float* __restrict__ L, const NetOff& o, const P3 (&xp)[NT],
+                                           Pipe<NT>& st) {
+  f32x16 b;
+  bias_init(b, L, o.b);
+  const P3 w1 = ld_split8(L, o.w1);
+#pragma unroll
+  for (int j = 0; j < NT; j++) {
+    const f32x16 a1 = mfma6(w1, xp[j], b);
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        split_pair(relu(a1[8 * t + 2 * k]), relu(a1[8 * t + 2 * k + 1]), st.h1[0][j][t], k);
+  }
+  st.raw[0][0] = ld4(L, w2_frag(o, 0)); st.raw[0][1] = ld4(L, w2_frag(o, 0) + 4);
+  st.raw[1][0] = ld4(L, w2_frag(o, 1)); st.raw[1][1] = ld4(L, w2_frag(o, 1) + 4);
+  const float v[8] = {st.raw[0][0].x, st.raw[0][0].y, st.raw[0][0].z, st.raw[0][0].w,
+                      st.raw[0][1].x, st.raw[0][1].y, st.raw[0][1].z, st.raw[0][1].w};
+  st.w = split8(v);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// one net's 32 layer-2 steps (+ layer 1 of its blocks 1..3, and with NEXT the next net's block 0
+// and first fragments), then its head
+template <int NOUT, int NT, bool NEXT>
+__device__ __forceinline__ void net_core(const float* __restrict__ L, const NetOff& o, const NetOff& on,
+                                         const P3 (&xp)[NT], Pipe<NT>& st, float (&out)[NT][NOUT]) {
+  const int h = (threadIdx.x >> 5) & 1;
   f32x16 acc[4][NT];
 #pragma unroll
   for (int m = 0; m < 4; m++) {
-    bias_init(acc[m][0], L, ob + B_F + m * 32);
+    bias_init(acc[m][0], L, o.b + B_F + m * 32);
 #pragma unroll
     for (int j = 1; j < NT; j++) acc[m][j] = acc[m][0];
   }
-  // W2 fragment of global k-step g = 8n + 4t + m
-  auto frag = [&](int g) { return o2 + (((g & 3) * 4 + (g >> 3)) * 2 + ((g >> 2) & 1)) * 512; };
-  P3 h1[2][NT][2];  // relu(h1) pieces of blocks n (buffer n & 1) and n + 1
-  {
-    f32x16 b;
-    bias_init(b, L, ob);
-    const P3 w1 = ld_split8(L, o1);
-#pragma unroll
-    for (int j = 0; j < NT; j++) {
-      const f32x16 a1 = mfma6(w1, xp[j], b);
-      relu_split<NT>(a1, 0, h1[0][j][0]);
-      relu_split<NT>(a1, 1, h1[0][j][1]);
-    }
-  }
-  float4 raw[2][2];  // W2 fragments read ahead (ring of two steps)
-  raw[0][0] = ld4(L, frag(0)); raw[0][1] = ld4(L, frag(0) + 4);
-  raw[1][0] = ld4(L, frag(1)); raw[1][1] = ld4(L, frag(1) + 4);
-  P3 w;
-  {
-    const float v[8] = {raw[0][0].x, raw[0][0].y, raw[0][0].z, raw[0][0].w,
-                        raw[0][1].x, raw[0][1].y, raw[0][1].z, raw[0][1].w};
-    w = split8(v);
-  }
-  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int n = 0; n < 4; n++) {
     const int cb = n & 1, nb = cb ^ 1;
+    const bool pre = n < 3 || NEXT;          // layer 1 of the next block during this one
+    const NetOff& ol = n < 3 ? o : on;       // whose next block
+    const int nn = n < 3 ? n + 1 : 0;
     P3 w1n;
     f32x16 b1n, a1n[NT];
 #pragma unroll
     for (int s = 0; s < 8; s++) {
       const int g = 8 * n + s, t = s >> 2, m = s & 3;
-      if (g + 2 < 32) {  // read step g + 2's fragment into the slot step g's split just freed
-        raw[g & 1][0] = ld4(L, frag(g + 2));
-        raw[g & 1][1] = ld4(L, frag(g + 2) + 4);
+      if (g + 2 < 32 || NEXT) {  // read step g + 2's fragment into the slot step g's split just freed
+        const int f = g + 2 < 32 ? w2_frag(o, g + 2) : w2_frag(on, g + 2 - 32);
+        st.raw[g & 1][0] = ld4(L, f);
+        st.raw[g & 1][1] = ld4(L, f + 4);
       }
 #pragma unroll
-      for (int j = 0; j < NT; j++) acc[m][j] = mfma6(w, h1[cb][j][t], acc[m][j]);
-      if (n < 3 && s == 1) {
+      for (int j = 0; j < NT; j++) acc[m][j] = mfma6(st.w, st.h1[cb][j][t].p(), acc[m][j]);
+      if (pre && s == 1) {
 #pragma unroll
         for (int j = 0; j < NT; j++) a1n[j] = mfma6(w1n, xp[j], b1n);
       }
       P3 wn;
-      if (g + 1 < 32) {
-        const float4 r0 = raw[(g + 1) & 1][0], r1 = raw[(g + 1) & 1][1];
+      if (g + 1 < 32 || NEXT) {
+        const float4 r0 = st.raw[(g + 1) & 1][0], r1 = st.raw[(g + 1) & 1][1];
         const float v[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
         wn = split8(v);
       }
-      if (n < 3 && s == 0) {
-        bias_init(b1n, L, ob + (n + 1) * 32);
-        w1n = ld_split8(L, o1 + (n + 1) * 512);
+      if (pre && s == 0) {
+        bias_init(b1n, L, ol.b + nn * 32);
+        w1n = ld_split8(L, ol.w1 + nn * 512);
       }
-      if (n < 3 && s >= 3 && s <= 6) {
-        const int u = s - 3;  // tile u >> 1, half u & 1 (NT = 1: halves at s = 3, 4)
-        if ((u >> 1) < NT) relu_split<NT>(a1n[u >> 1], u & 1, h1[nb][u >> 1][u & 1]);
+      if (pre && s >= 2) {  // pair-chunks c = 0..15 (tile c >> 3, half (c >> 2) & 1, pair c & 3) over s = 2..7
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+          if (2 + (c * 6) / 16 != s || (c >> 3) >= NT) continue;
+          const int j = c >> 3, tt = (c >> 2) & 1, k = c & 3;
+          split_pair(relu(a1n[j][8 * tt + 2 * k]), relu(a1n[j][8 * tt + 2 * k + 1]), st.h1[nb][j][tt], k);
+        }
       }
+#if QD_NF_VPG > 0
 #pragma unroll
       for (int q = 0; q < 6 * NT; q++) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, QD_NF_VPG, 0);
       }
+#endif
       __builtin_amdgcn_sched_barrier(0);
-      if (g + 1 < 32) w = wn;
+      if (g + 1 < 32 || NEXT) st.w = wn;
     }
   }
   float part[NT][NOUT];
 #pragma unroll
   for (int j = 0; j < NT; j++)
 #pragma unroll
-    for (int o = 0; o < NOUT; o++) part[j][o] = 0.f;
+    for (int q = 0; q < NOUT; q++) part[j][q] = 0.f;
 #pragma unroll
   for (int m = 0; m < 4; m++) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) head_part<NOUT, NT>(L, acc[m], m, i, o3, part);
+    for (int i = 0; i < 16; i++) head_part<NOUT, NT>(L, acc[m], m, i, o.w3, part);
     __builtin_amdgcn_sched_barrier(0);  // one block's accumulators in VGPRs at a time
   }
   // lanes l and l ^ 32 hold the two halves of the same env's neurons; both lanes form the same sum
 #pragma unroll
   for (int j = 0; j < NT; j++)
 #pragma unroll
-    for (int o = 0; o < NOUT; o++) {
-      const float other = __shfl_xor(part[j][o], 32);
-      out[j][o] = ((h ? other : part[j][o]) + (h ? part[j][o] : other)) + L[o3 - 4 * h + NOUT * 128 + o];
+    for (int q = 0; q < NOUT; q++) {
+      const float other = __shfl_xor(part[j][q], 32);
+      out[j][q] = ((h ? other : part[j][q]) + (h ? part[j][q] : other)) + L[o.w3 - 4 * h + NOUT * 128 + q];
     }
+}
+
+// one net (image at L): NOUT = ACT for the actor, 1 for the critic
+template <int NOUT, int NT>
+__device__ __forceinline__ void net_forward(const float* __restrict__ L, const float (&xq)[NT][8],
+                                            float (&out)[NT][NOUT]) {
+  P3 xp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; j++) xp[j] = split8(xq[j]);
+  const NetOff o = net_off(0);
+  Pipe<NT> st;
+  pipe_start<NT>(L, o, xp, st);
+  net_core<NOUT, NT, false>(L, o, o, xp, st, out);
+}
+
+// actor (image at L) then critic (at L + ACTOR_F) in one pipeline: the same bits as two net_forward
+// calls (every tile's operations and their order are the same)
+template <int NT>
+__device__ __forceinline__ void net_forward2(const float* __restrict__ L, const float (&xq)[NT][8],
+                                             float (&mean)[NT][ACT], float (&val)[NT][1]) {
+  P3 xp[NT];
+#pragma unroll
+  for (int j = 0; j < NT; j++) xp[j] = split8(xq[j]);
+  const NetOff oa = net_off(0), oc = net_off(ACTOR_F);
+  Pipe<NT> st;
+  pipe_start<NT>(L, oa, xp, st);
+  net_core<ACT, NT, true>(L, oa, oc, xp, st, mean);
+  net_core<1, NT, false>(L, oc, oc, xp, st, val);
 }
 
 // 152 KB global -> LDS per block: batches of 13 float4 loads in flight per thread (a serial

@@ -159,12 +159,12 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
       for (int k = 0; k < ACT; k++) mean[j][k] = xb[j][k];
     }
 #else
-    net_forward<ACT, NT>(lds, xb, mean);
 #if defined(QD_ROLL_NOCRITIC)
+    net_forward<ACT, NT>(lds, xb, mean);
 #pragma unroll
     for (int j = 0; j < NT; j++) val[j][0] = mean[j][0];
 #else
-    net_forward<1, NT>(lds + ACTOR_F, xb, val);
+    net_forward2<NT>(lds, xb, mean, val);
 #endif
 #endif
     float z[ACT] = {0.f, 0.f, 0.f, 0.f};
