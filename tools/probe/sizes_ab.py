@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Profiling tool (not product): the step kernel at N envs under several library / form settings,
+one process each (env overrides as KEY=VAL, a library path as LIB=path). Graph-replayed launches,
+HIP events (tools/lanes_sweep.run), best of 3. Usage: sizes_ab.py N "KEY=VAL ..." ["..."]"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    if sys.argv[1] == "child":
+        sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from uav_reinforcement_learning_control_amd import _native as N
+        if os.environ.get("LIB"):
+            N.LIB_PATH = os.environ["LIB"]
+        from lanes_sweep import run
+        lanes = int(os.environ.get("QUADENV_LANES", "1"))
+        n = int(sys.argv[2])
+        t = min(run(lanes, n, steps=400) for _ in range(3))
+        print(f"{sys.argv[3]:40s} n={n}: {t:.2f} us = {278 * n / t / 1e3:.0f} GB/s", flush=True)
+        return
+    n = sys.argv[1]
+    for spec in sys.argv[2:]:
+        env = dict(os.environ)
+        for kv in spec.split():
+            k, v = kv.split("=", 1)
+            env[k] = v
+        r = subprocess.run([sys.executable, __file__, "child", n, spec], capture_output=True, text=True, timeout=300, env=env)
+        print(r.stdout.strip() or r.stderr.strip()[-400:], flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -177,6 +177,24 @@ __device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, s16x8(__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7)));
 }
 
+// QD_LPROBE (tools/probe/probe_learner.py builds only, never the product): the dump build records
+// per-wave s_memtime stamps at the phase boundaries of round 2 into g.dump instead of the hidden
+// pre-activations (sched barriers around each stamp: the probe build is slower; use the shares)
+#if defined(QD_LPROBE)
+#define LP(k)                                        \
+  do {                                               \
+    if (DUMP && rd == 2) {                           \
+      __builtin_amdgcn_sched_barrier(0);             \
+      stp[k] = __builtin_amdgcn_s_memtime();         \
+      __builtin_amdgcn_sched_barrier(0);             \
+    }                                                \
+  } while (0)
+#define LP_DUMP(x) ((void)0)
+#else
+#define LP(k) ((void)0)
+#define LP_DUMP(x) x
+#endif
+
 template <int NOUT, bool DUMP = false>
 __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int blk) {
   const NetW& W = NOUT == ACT ? g.actor : g.critic;
@@ -300,8 +318,12 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   int64_t next_row = index_of(1);
   __syncthreads();
 
+#if defined(QD_LPROBE)
+  uint64_t stp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
   for (int rd = 0; rd < rounds; rd++) {
     const int base = s0 + rd * RND;
+    LP(0);
     char* const XO = L + B_XO + (rd & 1) * 3 * XIMG;
     float* const SCI = Lf + B_SC / 4 + (rd & 1) * RND * 8;
     if (tid < 3 * RND) {
@@ -326,6 +348,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
     for (int t = 0; t < 2; t++) valid[t] = base + 32 * t + l32 < s1;
     X3_BAR();  // B1: observation image complete; the previous round's readers are done
+    LP(1);
 
     // ---- L1 (E form): h1^T block w of both tiles -> H1 pieces
 #pragma unroll
@@ -338,8 +361,8 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       for (int p = 0; p < 3; p++) xb.p[p] = rd16(XO, p * XIMG + (32 * t + l32) * XROW + 16 * h);
       acc = mma3(w1x, xb, acc);
       if constexpr (DUMP) {
-        if (valid[t])
-          for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 0, 32 * w + acc_row(r, h), acc[r]);
+        LP_DUMP(if (valid[t])
+          for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 0, 32 * w + acc_row(r, h), acc[r]));
       }
 #pragma unroll
       for (int gg = 0; gg < 4; gg++) {  // registers 4gg.. = neurons 32w + 8gg + 4h + 0..3
@@ -351,6 +374,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
     X3_BAR();  // B2: H1 image complete
+    LP(2);
 
 #if !defined(QD_X3_NOL2)
     // ---- L2 (E form): h2^T block w, A = W2 rows (registers), B = H1 row reads
@@ -385,10 +409,11 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     f32x16 h2[2];
     for (int r = 0; r < 16; r++) { h2[0][r] = Lf[r]; h2[1][r] = Lf[r + 16]; }
 #endif
+    LP(3);
     if constexpr (DUMP) {
-      for (int t = 0; t < 2; t++)
+      LP_DUMP(for (int t = 0; t < 2; t++)
         if (valid[t])
-          for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 1, 32 * w + acc_row(r, h), h2[t][r]);
+          for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 1, 32 * w + acc_row(r, h), h2[t][r]));
     }
     // head partial sums over the wave's 32 neurons (the two lane halves hold 16 each)
 #pragma unroll
@@ -411,6 +436,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
     X3_BAR();  // B3: head partials complete
+    LP(4);
 
     // ---- per-row loss terms and dL/d(head output) (every wave, identical arithmetic)
     float d[2][NOUT];
@@ -461,6 +487,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         }
       }
     }
+    LP(5);
     // ---- dh2 (E form) -> DH2 pieces; relu(h2) -> f32 image; db2 per lane
 #pragma unroll
     for (int t = 0; t < 2; t++) {
@@ -487,6 +514,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
     X3_BAR();  // B4: DH2, relu(h2) and dL/dmean images complete
+    LP(6);
 
 #if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
@@ -529,6 +557,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
 #endif
+    LP(7);
     // ---- dW3 columns 32w.. (f32 16x16x4: A = dL/dmean^T (rows = outputs), B = relu(h2) rows)
 #pragma unroll
     for (int s = 0; s < 16; s++) {
@@ -540,6 +569,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         dW3[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, hv, dW3[b], 0, 0, 0);
       }
     }
+    LP(8);
 #if !defined(QD_X3_NODH1)
     // ---- dh1 (R form) = relu'(h1) . (dh2 W2[:, block w]); then the dW1 slab (+ db1 in column 12)
     f32x16 dh1[2];
@@ -568,6 +598,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         if (s < 7) { b = bn; a[0] = an[0]; a[1] = an[1]; }
       }
     }
+    LP(9);
 #pragma unroll
     for (int t = 0; t < 2; t++) {
       f32x16& acc = dh1[t];
@@ -599,7 +630,15 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
   #endif
+    LP(10);
 }
+#if defined(QD_LPROBE)
+  if (DUMP && lane == 0) {
+    uint64_t* o = reinterpret_cast<uint64_t*>(g.dump) + (size_t(blockIdx.x) * 4 + size_t(w)) * 16;
+    for (int k = 0; k < 11; k++) o[k] = stp[k];
+    o[15] = NOUT;
+  }
+#endif
 
   // ---- block partials in the parameter layout
   float* P = g.part + size_t(blk + (NOUT == ACT ? 0 : g.nb)) * PSTRIDE;
