@@ -19,7 +19,22 @@ def main():
         lanes = int(os.environ.get("QUADENV_LANES", "1"))
         n = int(sys.argv[2])
         t = min(run(lanes, n, steps=400) for _ in range(3))
-        print(f"{sys.argv[3]:40s} n={n}: {t:.2f} us = {278 * n / t / 1e3:.0f} GB/s", flush=True)
+        dg = ""
+        if os.environ.get("DIGEST"):  # every output of 40 stepped steps: forms must agree bit for bit
+            import hashlib
+            import torch
+            from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+            e = QuadVecEnv(n, device="cuda:0", seed=3)
+            e.reset()
+            h = hashlib.sha256()
+            for k in range(40):
+                obs, rew, term, trunc, inf = e.step(e.random_actions(k))
+                for x in (obs, rew, term, trunc, inf["terminal_observation"]):
+                    h.update(x.cpu().numpy().tobytes())
+            for v in e.get_state().values():
+                h.update(v.tobytes())
+            dg = " digest " + h.hexdigest()[:16]
+        print(f"{sys.argv[3]:40s} n={n}: {t:.2f} us = {278 * n / t / 1e3:.0f} GB/s{dg}", flush=True)
         return
     n = sys.argv[1]
     for spec in sys.argv[2:]:
