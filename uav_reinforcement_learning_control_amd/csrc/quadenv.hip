@@ -296,6 +296,9 @@ __device__ __forceinline__ void step_body(const KConsts<float>& K, KParams p, co
 // measured equal (5.84-5.87 vs 5.83-5.87 us) and 128 slower (6.10), so batches above H_SMALL keep
 // 256 (profiles/r02/ab_step_h_block.txt).
 constexpr int H_SMALL = 32768;
+#ifndef QD_H_PRE
+#define QD_H_PRE 1  // Philox blocks of the helper's reset draw issued before barrier (C): 1 measured best (below)
+#endif
 constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
 constexpr int HCTL = 9;   // floats per env from the control helper: Fsum, taum 3, volt, bad ctrl, rint 3
 template <int KIND, bool CTBR, int HB>
@@ -356,13 +359,23 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
             make_float4(float(c.F[0]), float(c.F[1]), float(c.F[2]), float(c.F[3])));
       if (out.voltage_scale) sto(out.voltage_scale, o, float(c.vs));
     }
+    // (R) env i's next reset, into H[f][l]: the first PRE Philox blocks before barrier (C), at
+    // normal priority, in the slack the helper has while the step wave accumulates forward_base
+    constexpr int PRE = QD_H_PRE;
+    float u16[16];
+    if (PRE > 0) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (uint32_t b = 0; b < uint32_t(PRE); b++) {
+      uint32_t cw[4];
+      reset_block(p.seed, p.gid_base + uint64_t(i), ep, b, cw);
+#pragma unroll
+      for (int j = 0; j < 4; j++) u16[4 * b + j] = u01(cw[j]);
+    }
     __syncthreads();  // (C) the control results are staged
     QD_STAMP(stamps, 3);
     __builtin_amdgcn_s_setprio(0);
-    // (R) env i's next reset, into H[f][l]
-    float u16[16];
 #pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
+    for (uint32_t b = uint32_t(PRE); b < 4; b++) {
       uint32_t cw[4];
       reset_block(p.seed, p.gid_base + uint64_t(i), ep, b, cw);
 #pragma unroll
