@@ -105,6 +105,20 @@ QD_HD float q_exp(float x) { return expf(x); }
 QD_HD double q_exp(double x) { return exp(x); }
 QD_HD void q_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 
+// int(q) & 3 of an integral float with v_cvt_i32_f32's semantics (saturating, NaN -> 0) on the
+// host as well: there the plain conversion of a diverged state's huge or NaN angle is undefined
+// behaviour (found by UBSan, tools/san); the device keeps the one conversion instruction
+QD_HD int quadrant_of(float q) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return int(q) & 3;
+#else
+  if (!(q == q)) return 0;
+  if (q >= 2147483648.0f) return 3;  // INT_MAX & 3
+  if (q < -2147483648.0f) return 0;  // INT_MIN & 3
+  return int(q) & 3;
+#endif
+}
+
 // sin/cos: Cody-Waite reduction by pi/2 with two constants (exact to ~1e-10 rad for
 // |x| < 1e5; hinge angles accumulate but stay far below that), Taylor polynomials on
 // [-pi/4, pi/4] (truncation < 2.5e-8), quadrant select.
@@ -118,7 +132,7 @@ QD_HD void q_sincos(float x, float* s, float* c) {
   const float sn = fmaf(r, sp, r);
   const float cp = fmaf(r2, fmaf(r2, fmaf(r2, fmaf(r2, fmaf(r2, -2.7557319224e-7f, 2.4801587302e-5f),
                                                    -1.3888888889e-3f), 4.1666666667e-2f), -0.5f), 1.0f);
-  const int qi = int(q) & 3;
+  const int qi = quadrant_of(q);
   const float a = (qi & 1) ? cp : sn;
   const float b = (qi & 1) ? sn : cp;
   *s = (qi & 2) ? -a : a;
