@@ -41,12 +41,17 @@ struct GArgs {
   int32_t nbc, per_block_c;         // critic: nbc blocks of per_block_c rows
   float clip, inv_batch, vf_coef;
   float* dump;  // diagnostics only (k_ppo_grad*_dump): [2 nets][batch][256] hidden pre-activations
+  const void* wimg;  // bf16x3 form: the W2 fragments of every wave as bf16 pieces (k_split_w2, WIMG_BYTES)
 };
 
 struct Layout {
   int nb, per_block, nbc, per_block_c;
-  int64_t part_bytes, adv_bytes;
+  int64_t part_bytes, adv_bytes, wimg_bytes;
 };
+
+// the bf16x3 form's pre-split W2 image (learner_x3.hip k_split_w2): 2 nets x 4 waves x 2 uses x
+// 8 k-steps x 3 pieces x 64 lanes x 16 bytes, after the partial image in the workspace
+constexpr int64_t WIMG_BYTES = int64_t(2) * 4 * 2 * 8 * 3 * 64 * 16;
 
 // Block split of a minibatch of `batch` rows: the two nets share the 2 * MAX_NB block slots in
 // proportion `actor_share` / 1000 (a critic round costs less than an actor round: no log-prob /
@@ -63,12 +68,13 @@ inline Layout layout_of(int32_t batch, int actor_share) {
   l.per_block_c = ((rounds + l.nbc - 1) / l.nbc) * RND;
   l.part_bytes = int64_t(slots) * PSTRIDE * int64_t(sizeof(float));
   l.adv_bytes = int64_t(ADV_BLOCKS) * 2 * int64_t(sizeof(double));
+  l.wimg_bytes = WIMG_BYTES;
   return l;
 }
 
 // the bf16x3 form (learner_x3.hip): its actor share and launcher
 int x3_actor_share();
-int launch_ppo_grad_x3(const GArgs& g, hipStream_t s);
+int launch_ppo_grad_x3(const GArgs& g, hipStream_t s);  // k_split_w2 + k_ppo_grad_x3
 int launch_ppo_grad_x3_dump(const GArgs& g, hipStream_t s);
 
 // Diagnostics (quad_ppo_hidden): the kernels' own hidden pre-activations of minibatch row `pos`

@@ -637,7 +637,7 @@ extern "C" {
 int64_t quad_ppo_workspace_bytes(int32_t batch) {
   if (batch < 1) return 0;
   const Layout l = layout_of(batch, ACTOR_SHARE);  // the partial image is sized for every split
-  return l.adv_bytes + l.part_bytes;
+  return l.adv_bytes + l.part_bytes + l.wimg_bytes;
 }
 
 // 1: the bf16x3 form (k_ppo_grad_x3, default), 0: the f32-input MFMA form (k_ppo_grad);
@@ -671,7 +671,8 @@ int ppo_grad_impl(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   const bool x3 = quad_ppo_grad_form() == 1;
   const Layout l = layout_of(b->batch, x3 ? x3_actor_share() : ACTOR_SHARE);
   if (dump && int64_t(b->batch) * 2 * 256 * 4 > (int64_t(1) << 40)) return lfail(QUAD_EINVAL, "batch too large to dump");
-  if (workspace_bytes < l.adv_bytes + l.part_bytes) return lfail(QUAD_EINVAL, "workspace too small");
+  if (workspace_bytes < l.adv_bytes + l.part_bytes + (x3 ? l.wimg_bytes : 0))
+    return lfail(QUAD_EINVAL, "workspace too small");
   static bool opted[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return lfail(QUAD_EHIP, "hipGetDevice failed");
@@ -703,6 +704,7 @@ int ppo_grad_impl(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   g.batch = b->batch; g.nb = l.nb; g.per_block = l.per_block; g.nbc = l.nbc; g.per_block_c = l.per_block_c;
   g.clip = b->clip_range; g.inv_batch = 1.0f / float(b->batch); g.vf_coef = b->vf_coef;
   g.dump = dump;
+  g.wimg = static_cast<char*>(workspace) + l.adv_bytes + l.part_bytes;
   if (x3) {
     if (int rc = dump ? launch_ppo_grad_x3_dump(g, s) : launch_ppo_grad_x3(g, s)) return rc;
   } else if (dump) {

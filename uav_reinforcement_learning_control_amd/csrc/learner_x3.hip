@@ -14,13 +14,13 @@
 // Structure (per block: one net, 4 waves, wave w owns neurons 32w..32w+31 of both hidden layers,
 // rounds of 64 minibatch rows = two 32-row tiles; the loss math is learner.hip's):
 //   L1   h1^T = W1 x^T        E form (neurons in registers, rows on lanes)  -> H1 pieces image
-//   L2   h2^T = W2 h1^T       E form: A = W2 rows (registers), B = H1 row reads (ds_read_b128)
+//   L2   h2^T = W2 h1^T       E form: A = W2 rows (pre-split pieces from HBM, k_split_w2), B = H1 row reads
 //   head / loss / dL/dmean    VALU, as learner.hip
 //   dh2  E form               -> DH2 pieces image, relu(h2) -> f32 image (dW3)
 //   dW2  = dh2^T h1 (K = rows)  A = DH2, B = H1, both by transposed reads (ds_read_b64_tr_b16);
 //        db2 = dh2^T . ones from the same A fragments
 //   dW3  = dmean^T h2         f32 16x16x4 MFMA (small)
-//   dh1  R form (rows in registers): A = DH2 row reads, B = W2 columns (registers); relu'(h1)
+//   dh1  R form (rows in registers): A = DH2 row reads, B = W2 columns (pre-split pieces); relu'(h1)
 //        from the H1 image by transposed reads
 //   dW1  = dh1^T x            the dh1 accumulator split in registers is the A operand; B = the
 //        observation image by transposed reads; its column 12 is 1.0, so dW1's column 12 is db1
@@ -113,6 +113,16 @@ static_assert(2 * LB * 8 <= RND * SH * 4, "the advantage reduction aliases the r
 #else
 #define X3_PIPE(n_rd, n_mfma) ((void)0)
 #endif
+// the same with `n_vm` global loads (the pre-split weight pieces two k-steps ahead) issued first
+#if !defined(QD_X3_NOPIPE)
+#define X3_PIPE_V(n_vm, n_rd, n_mfma)                                           \
+  do {                                                                          \
+    __builtin_amdgcn_sched_group_barrier(0x020, (n_vm), 0);                     \
+    X3_PIPE(n_rd, n_mfma);                                                      \
+  } while (0)
+#else
+#define X3_PIPE_V(n_vm, n_rd, n_mfma) ((void)0)
+#endif
 
 __device__ __forceinline__ int soff(int row, int ch) { return RS * row + 16 * ch; }
 
@@ -162,6 +172,33 @@ __device__ __forceinline__ f32x16 mma3(const X3& a, const X3& b, f32x16 c) {
   c = mfma16(a.p[1], b.p[0], c);
   c = mfma16(a.p[0], b.p[1], c);
   return mfma16(a.p[0], b.p[0], c);
+}
+
+// The W2 fragments a wave multiplies with, as bf16 pieces in HBM (L2-resident, 96 KB per net),
+// split once per launch by k_split_w2: unit (16 bytes) of (net, wave w, use u, k-step s, piece p,
+// lane). Use 0 = A of L2: W2[n_own][kk]; use 1 = B of dh1: W2[kk][n_own]; kk = 8s + 64h + j for
+// lane half h, element j (n_own = 32w + lane % 32). Loading the pieces (3 dwordx4 per k-step)
+// replaces re-splitting f32 slices held in registers each round (~45 VALU per k-step and operand,
+// and the slices' 128 VGPRs); same pieces, so the same bits.
+__device__ __forceinline__ int wimg_unit(int net, int w, int u, int s, int p, int lane) {
+  return ((((net * 4 + w) * 2 + u) * 8 + s) * 3 + p) * 64 + lane;
+}
+static_assert(int64_t(2 * 4 * 2 * 8 * 3 * 64) * 16 == WIMG_BYTES, "pre-split image size");
+
+__global__ __launch_bounds__(64) void k_split_w2(const float* __restrict__ wa, const float* __restrict__ wc,
+                                                 bf16x8* __restrict__ img) {
+  const int b = blockIdx.x, s = b & 7, u = (b >> 3) & 1, w = (b >> 4) & 3, net = b >> 6;
+  const int lane = threadIdx.x, h = lane >> 5, n_own = 32 * w + (lane & 31);
+  const float* w1 = net ? wc : wa;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int kk = 8 * s + 64 * h + j;
+    v[j] = u == 0 ? w1[n_own * H + kk] : w1[kk * H + n_own];
+  }
+  const X3 x = split8(v);
+#pragma unroll
+  for (int p = 0; p < 3; p++) img[wimg_unit(net, w, u, s, p, lane)] = x.p[p];
 }
 
 __device__ __forceinline__ bf16x8 rd16(const char* L, int off) { return *reinterpret_cast<const bf16x8*>(L + off); }
@@ -223,7 +260,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   }
   const float adv_rden = 1.f / adv_den;
 
-  // ---- small weights in LDS; the wave's W1 / W2 fragments split in registers
+  // ---- small weights in LDS; the wave's W1 fragment split in registers
   for (int i = tid; i < H; i += LB) {
     Lf[B_B1 / 4 + i] = W.b0[i];
     Lf[B_B2 / 4 + i] = W.b1[i];
@@ -241,22 +278,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     for (int j = 0; j < 8; j++) v[j] = 8 * h + j < OBS ? W.w0[n_own * OBS + 8 * h + j] : 0.f;
     w1x = split8(v);
   }
-  // W2 slices in f32, split into pieces at each use (the split pieces of both would take 192 VGPRs).
-  // k order of the 128-deep products: at k-step s, lane half h holds k = 8s + 64h + j, i.e. chunk
-  // s + 8h of an image row, so lanes l and l + 32 read chunks 128 B apart (conflict-free b128 reads):
-  // wA[s][j] = W2[n_own][kk] (A of L2), wB[s][j] = W2[kk][n_own] (B of dh1), kk = 8s + 64h + j
-  float wA[8][8], wB[8][8];
-#pragma unroll
-  for (int s = 0; s < 8; s++) {
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      wA[s][j] = W.w1[n_own * H + 8 * s + 64 * h + j];
-      wB[s][j] = W.w1[(8 * s + 64 * h + j) * H + n_own];
-    }
-  }
-  // (the splits are loop-invariant: the compiler hoists them out of the round loop)
-#define SPLIT_A(s) split8(wA[s])
-#define SPLIT_B(s) split8(wB[s])
+  // this wave's pre-split W2 fragments (k_split_w2); the base is made opaque each round so the
+  // compiler cannot hoist the 48 loads out of the round loop (their 192 VGPRs would spill)
+  const int wunit0 = wimg_unit(NOUT == ACT ? 0 : 1, w, 0, 0, 0, lane);
   float ls[ACT], sd[ACT], isd[ACT];  // isd: the row loop multiplies (a full-precision division is ~10 VALU)
   if constexpr (NOUT == ACT) {
 #pragma unroll
@@ -323,6 +347,18 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #endif
   for (int rd = 0; rd < rounds; rd++) {
     const int base = s0 + rd * RND;
+    uint64_t wbase = reinterpret_cast<uint64_t>(g.wimg);
+    asm volatile("" : "+s"(wbase));
+    typedef __attribute__((address_space(1))) const bf16x8 gbf16x8;  // global, not flat: no lgkmcnt
+    gbf16x8* const WI = reinterpret_cast<gbf16x8*>(wbase) + wunit0;
+    auto ldw = [&](int u, int s) {
+      X3 x;
+#pragma unroll
+      for (int p = 0; p < 3; p++) x.p[p] = WI[((u * 8 + s) * 3 + p) * 64];
+      return x;
+    };
+#define WLOAD(u, s) ldw(u, s)
+    const X3 wa0 = WLOAD(0, 0), wa1 = WLOAD(0, 1);  // L2's first two k-steps: in flight through L1
     LP(0);
     char* const XO = L + B_XO + (rd & 1) * 3 * XIMG;
     float* const SCI = Lf + B_SC / 4 + (rd & 1) * RND * 8;
@@ -342,8 +378,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       *reinterpret_cast<float4*>(SCI + srow * 8) = pf;
       SCI[srow * 8 + 4] = pfs[0]; SCI[srow * 8 + 5] = pfs[1]; SCI[srow * 8 + 6] = pfs[2];
     }
-    gather(next_row);           // round rd + 1, in flight during this round
-    next_row = index_of(rd + 2);
     bool valid[2];
 #pragma unroll
     for (int t = 0; t < 2; t++) valid[t] = base + 32 * t + l32 < s1;
@@ -377,38 +411,44 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     LP(2);
 
 #if !defined(QD_X3_NOL2)
-    // ---- L2 (E form): h2^T block w, A = W2 rows (registers), B = H1 row reads
+    // ---- L2 (E form): h2^T block w, A = W2 rows (pre-split pieces), B = H1 row reads
     f32x16 h2[2];
 #pragma unroll
     for (int r = 0; r < 16; r++) h2[0][r] = Lf[B_B2 / 4 + 32 * w + acc_row(r, h)];
     h2[1] = h2[0];
-    {  // software pipeline: step s's MFMAs with step s + 1's reads and weight split in flight
-      X3 a = SPLIT_A(0), b[2];
+    {  // software pipeline: step s's MFMAs with step s + 1's reads and step s + 2's weight pieces in flight
+      X3 a = wa0, an = wa1, b[2];
 #pragma unroll
       for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int p = 0; p < 3; p++) b[t].p[p] = rd16(L, B_H1P + p * IMG + soff(32 * t + l32, 8 * h));
 #pragma unroll
       for (int s = 0; s < 8; s++) {
-        X3 an, bn[2];
+        X3 ann, bn[2];
+        if (s < 6) ann = WLOAD(0, s + 2);
         if (s < 7) {
 #pragma unroll
           for (int t = 0; t < 2; t++)
 #pragma unroll
             for (int p = 0; p < 3; p++) bn[t].p[p] = rd16(L, B_H1P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
-          an = SPLIT_A(s + 1);
         }
 #pragma unroll
         for (int t = 0; t < 2; t++) h2[t] = mma3(a, b[t], h2[t]);
-        if (s < 7) X3_PIPE(6, 12);
+        if (s < 6) X3_PIPE_V(3, 6, 12);
+        else if (s < 7) X3_PIPE(6, 12);
         X3_SB();
-        if (s < 7) { a = an; b[0] = bn[0]; b[1] = bn[1]; }
+        if (s < 7) { a = an; an = ann; b[0] = bn[0]; b[1] = bn[1]; }
       }
     }
 #else
     f32x16 h2[2];
     for (int r = 0; r < 16; r++) { h2[0][r] = Lf[r]; h2[1][r] = Lf[r + 16]; }
 #endif
+    // Row staging for round rd + 1, issued after L2's weight-piece loads: vmcnt retires in issue
+    // order, so a gather issued before them would expose its HBM latency at L2's first wait; from
+    // here it has the rest of the round (the dh1 pieces are waited ~10k cycles later)
+    gather(next_row);
+    next_row = index_of(rd + 2);
     LP(3);
     if constexpr (DUMP) {
       LP_DUMP(for (int t = 0; t < 2; t++)
@@ -514,6 +554,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
     X3_BAR();  // B4: DH2, relu(h2) and dL/dmean images complete
+    const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);  // dh1's first two k-steps: in flight through dW2
     LP(6);
 
 #if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
@@ -575,27 +616,28 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     f32x16 dh1[2];
 #pragma unroll
     for (int r = 0; r < 16; r++) { dh1[0][r] = 0.f; dh1[1][r] = 0.f; }
-    {  // software pipeline as L2: A = DH2 row reads, B = split W2 columns
-      X3 b = SPLIT_B(0), a[2];
+    {  // software pipeline as L2: A = DH2 row reads, B = pre-split W2 columns
+      X3 b = wb0, bn = wb1, a[2];
 #pragma unroll
       for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int p = 0; p < 3; p++) a[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, 8 * h));
 #pragma unroll
       for (int s = 0; s < 8; s++) {
-        X3 bn, an[2];
+        X3 bnn, an[2];
+        if (s < 6) bnn = WLOAD(1, s + 2);
         if (s < 7) {
 #pragma unroll
           for (int t = 0; t < 2; t++)
 #pragma unroll
             for (int p = 0; p < 3; p++) an[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
-          bn = SPLIT_B(s + 1);
         }
 #pragma unroll
         for (int t = 0; t < 2; t++) dh1[t] = mma3(a[t], b, dh1[t]);
-        if (s < 7) X3_PIPE(6, 12);
+        if (s < 6) X3_PIPE_V(3, 6, 12);
+        else if (s < 7) X3_PIPE(6, 12);
         X3_SB();
-        if (s < 7) { b = bn; a[0] = an[0]; a[1] = an[1]; }
+        if (s < 7) { b = bn; bn = bnn; a[0] = an[0]; a[1] = an[1]; }
       }
     }
     LP(9);
@@ -714,9 +756,19 @@ __global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3_net(GArgs g) {
 }  // namespace
 
 #ifndef QD_LRN_X3_ACTOR_SHARE
-#define QD_LRN_X3_ACTOR_SHARE 580  // measured (524,288 rows): 520 -> 0.96 ms, 540 -> 0.94-0.95, 580 -> 0.88-0.89, 600 -> 0.92, 620 -> 0.97
+// measured (524,288 rows), round 2: 520 -> 0.96 ms, 540 -> 0.94-0.95, 580 -> 0.88-0.89, 600 -> 0.92;
+// round 3 with the pre-split W2 pieces (the actor round dropped 29.8k -> 24.3k cycles, the critic
+// 23.0k -> 22.0k): 500 -> 795 us, 520 -> 782, 540 -> 781, 560 -> 808, 580 -> 829 (old kernel 811)
+#define QD_LRN_X3_ACTOR_SHARE 530
 #endif
-int x3_actor_share() { return QD_LRN_X3_ACTOR_SHARE; }
+int x3_actor_share() {  // QUADENV_X3_ACTOR_SHARE (per mille, 100..900): A/B sweeps only
+  static const int v = [] {
+    const char* e = std::getenv("QUADENV_X3_ACTOR_SHARE");
+    const int x = e ? std::atoi(e) : 0;
+    return x >= 100 && x <= 900 ? x : QD_LRN_X3_ACTOR_SHARE;
+  }();
+  return v;
+}
 
 int launch_ppo_grad_x3(const GArgs& g, hipStream_t s) {
   static bool opted[64] = {};
@@ -728,6 +780,9 @@ int launch_ppo_grad_x3(const GArgs& g, hipStream_t s) {
       return set_error(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     opted[dev] = true;
   }
+  hipLaunchKernelGGL(k_split_w2, dim3(128), dim3(64), 0, s, g.actor.w1, g.critic.w1,
+                     const_cast<bf16x8*>(static_cast<const bf16x8*>(g.wimg)));
+  if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_split_w2 launch failed");
   const char* sp = std::getenv("QUADENV_LEARNER_SPLIT");
   if (sp && std::atoi(sp) != 0) {
     static hipStream_t s2[64] = {};
@@ -765,6 +820,9 @@ int launch_ppo_grad_x3_dump(const GArgs& g, hipStream_t s) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_x3_dump), hipFuncAttributeMaxDynamicSharedMemorySize,
                           B_TOTAL) != hipSuccess)
     return set_error(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  hipLaunchKernelGGL(k_split_w2, dim3(128), dim3(64), 0, s, g.actor.w1, g.critic.w1,
+                     const_cast<bf16x8*>(static_cast<const bf16x8*>(g.wimg)));
+  if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_split_w2 launch failed");
   hipLaunchKernelGGL(k_ppo_grad_x3_dump, dim3(g.nb + g.nbc), dim3(LB), B_TOTAL, s, g);
   if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3_dump launch failed");
   return QUAD_OK;
