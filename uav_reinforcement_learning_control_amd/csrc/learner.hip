@@ -465,23 +465,25 @@ struct RArgs {
   float inv_batch, ent_coef;
 };
 
-// one thread per (net, parameter): sum of the nb block partials in block order
+// one thread per (net, parameter): sum of the nb block partials in block order, in float64 (the
+// partials of a bias or head gradient are sums over disjoint row sets that largely cancel)
 __global__ __launch_bounds__(256) void k_ppo_reduce(RArgs a) {
   const int q = blockIdx.x * 256 + threadIdx.x;
   if (q >= 2 * PSTRIDE) return;
   const int net = q / PSTRIDE, p = q % PSTRIDE;
   const float* src = a.part + size_t(net) * a.nb * PSTRIDE + p;
   const int nb = net ? a.nbc : a.nb;
-  float s = 0.f;
+  double sd = 0.0;
   int b = 0;
   for (; b + 16 <= nb; b += 16) {  // 16 loads in flight per thread; summed in block order
     float v[16];
 #pragma unroll
     for (int u = 0; u < 16; u++) v[u] = src[size_t(b + u) * PSTRIDE];
 #pragma unroll
-    for (int u = 0; u < 16; u++) s += v[u];
+    for (int u = 0; u < 16; u++) sd += double(v[u]);
   }
-  for (; b < nb; b++) s += src[size_t(b) * PSTRIDE];
+  for (; b < nb; b++) sd += double(src[size_t(b) * PSTRIDE]);
+  const float s = float(sd);
   const QuadPolicyGrads& g = a.gr;
   if (p < P_B1) { (net ? g.vf_w0 : g.pi_w0)[p - P_W1] = s; return; }
   if (p < P_W2) { (net ? g.vf_b0 : g.pi_b0)[p - P_B1] = s; return; }

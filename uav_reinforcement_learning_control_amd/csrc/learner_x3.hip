@@ -16,10 +16,11 @@
 //   L1   h1^T = W1 x^T        E form (neurons in registers, rows on lanes)  -> H1 pieces image
 //   L2   h2^T = W2 h1^T       E form: A = W2 rows (pre-split pieces from HBM, k_split_w2), B = H1 row reads
 //   head / loss / dL/dmean    VALU, as learner.hip
-//   dh2  E form               -> DH2 pieces image, relu(h2) -> f32 image (dW3)
+//   dh2  E form               -> DH2 pieces image; dW3 += dmean^T relu(h2) per lane (f32 FMAs in
+//        registers, rows = lanes; the 32 lanes of each half are summed once at the end of the launch)
 //   dW2  = dh2^T h1 (K = rows)  A = DH2, B = H1, both by transposed reads (ds_read_b64_tr_b16);
-//        db2 = dh2^T . ones from the same A fragments
-//   dW3  = dmean^T h2         f32 16x16x4 MFMA (small)
+//        db2 per lane in f32 (VALU adds of the unsplit dh2, summed over the lanes at the end): the
+//        MFMA-with-ones form accumulated over K = rows with the bf16 MFMA's truncating sums
 //   dh1  R form (rows in registers): A = DH2 row reads, B = W2 columns (pre-split pieces); relu'(h1)
 //        from the H1 image by transposed reads
 //   dW1  = dh1^T x            the dh1 accumulator split in registers is the A operand; B = the
@@ -59,23 +60,20 @@ struct X3h {
 // LDS (bytes)
 constexpr int RS = 272;                        // row stride (bytes) of the bf16 images: 256 + 16
 constexpr int IMG = RND * RS;                  // one [64 row][128 neuron] bf16 piece
-constexpr int SH = 130;                        // row stride (floats) of the f32 relu(h2) image
 constexpr int XROW = 32;                       // observation image row: 12 features, 1.0, 3 zeros (bf16)
 constexpr int XIMG = RND * XROW;
 constexpr int B_H1P = 0;                       // 3 pieces
 constexpr int B_DH2P = B_H1P + 3 * IMG;        // 3 pieces
-constexpr int B_H2 = B_DH2P + 3 * IMG;         // f32 [64][SH]
-constexpr int B_XO = B_H2 + RND * SH * 4;      // [2 round buffers][3 pieces][64][16] bf16
+constexpr int B_XO = B_DH2P + 3 * IMG;         // [2 round buffers][3 pieces][64][16] bf16
 constexpr int B_ZERO = B_XO + 2 * 3 * XIMG;    // 64 zero bytes: dW1's padded columns 16..31
 constexpr int B_SC = B_ZERO + 64;              // f32 [2][64][8] row scalars: action 4, old logp, adv, return
-constexpr int B_DM = B_SC + 2 * RND * 8 * 4;   // f32 [64][4] dL/dmean (dL/dV in column 0)
-constexpr int B_PART = B_DM + RND * 16;        // f32 [4 waves][64][4] head partial sums
+constexpr int B_PART = B_SC + 2 * RND * 8 * 4; // f32 [4 waves][64][4] head partial sums
 constexpr int B_W3T = B_PART + 4 * RND * 16;   // f32 [128][4] head weights, neuron-major
 constexpr int B_B1 = B_W3T + H * 16, B_B2 = B_B1 + H * 4;
 constexpr int B_TOTAL = B_B2 + H * 4;          // 162,368 B
 static_assert(B_TOTAL <= 160 * 1024, "LDS budget");
-static_assert(B_XO % 16 == 0 && B_SC % 16 == 0 && B_W3T % 16 == 0 && B_H2 % 16 == 0, "alignment");
-static_assert(2 * LB * 8 <= RND * SH * 4, "the advantage reduction aliases the relu(h2) image");
+static_assert(B_XO % 16 == 0 && B_SC % 16 == 0 && B_W3T % 16 == 0, "alignment");
+static_assert(2 * LB * 8 <= 3 * IMG, "the advantage reduction aliases the DH2 image");
 
 // byte offset of 16-byte chunk `ch` of image row `row`. Padded rows (68 dwords) instead of an XOR
 // swizzle: every address is affine in the k-step / tile / block indices, so each read takes one
@@ -201,6 +199,24 @@ __global__ __launch_bounds__(64) void k_split_w2(const float* __restrict__ wa, c
   for (int p = 0; p < 3; p++) img[wimg_unit(net, w, u, s, p, lane)] = x.p[p];
 }
 
+// the same product with the five small terms in their own accumulator `sm` (magnitude ~2^-8 of the
+// sum): the bf16 MFMA truncates what falls below its f32 result (tools/diag/mfma_rounding.hip, a
+// small negative bias per instruction); five tiny-term MFMAs per k-step onto the full-size running
+// sum gave the forward outputs a systematic bias of up to ~48 ulp over a 128-deep product, which
+// the minibatch sums of the bias / head gradients accumulate linearly. The caller adds sm once.
+__device__ __forceinline__ void mma3s(const X3& a, const X3& b, f32x16& big, f32x16& sm) {
+#if defined(QD_X3_ONEACC)  // A/B builds only: the single-accumulator order
+  big = mma3(a, b, big);
+  return;
+#endif
+  sm = mfma16(a.p[2], b.p[0], sm);
+  sm = mfma16(a.p[1], b.p[1], sm);
+  sm = mfma16(a.p[0], b.p[2], sm);
+  sm = mfma16(a.p[1], b.p[0], sm);
+  sm = mfma16(a.p[0], b.p[1], sm);
+  big = mfma16(a.p[0], b.p[0], big);
+}
+
 __device__ __forceinline__ bf16x8 rd16(const char* L, int off) { return *reinterpret_cast<const bf16x8*>(L + off); }
 
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p addresses row q / columns 4p..4p+3 of a 4 x 16
@@ -245,7 +261,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   // ---- advantage statistics of the minibatch (actor): fixed-order tree over the pre-pass partials
   float adv_mu = 0.f, adv_den = 1.f;
   if (NOUT == ACT && g.adv_part) {
-    double* red = reinterpret_cast<double*>(L + B_H2);  // [2][LB], before the relu(h2) image is used
+    double* red = reinterpret_cast<double*>(L + B_DH2P);  // [2][LB], before the DH2 image is used
     red[tid] = g.adv_part[2 * tid];
     red[LB + tid] = g.adv_part[2 * tid + 1];
     __syncthreads();
@@ -288,22 +304,21 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   }
 
   // accumulators (whole launch)
-  f32x16 dW2[4], dW1;
-  f32x4 dW3[2];
-  f32x16 dB2;  // db2 of neuron 32w + acc_row(r, h) in register r (every column the same): dh2^T . ones
+  f32x16 dW2[4], dW1, dW1b, dW1s;  // dW1b / dW1s: the last round's dW1 (big / small terms)
+  float dW3[NOUT][16];  // per lane: sum over this lane's rows of dL/dout[k] * relu(h2) of register r's neuron
+  float dB2[16];  // per lane: sum over this lane's rows of dh2 of neuron 32w + acc_row(r, h)
 #pragma unroll
   for (int r = 0; r < 16; r++) {
-    dW1[r] = 0.f;
+    dW1[r] = dW1b[r] = dW1s[r] = 0.f;
 #pragma unroll
     for (int j = 0; j < 4; j++) dW2[j][r] = 0.f;
   }
 #pragma unroll
-  for (int r = 0; r < 4; r++) { dW3[0][r] = 0.f; dW3[1][r] = 0.f; }
+  for (int r = 0; r < 16; r++)
+#pragma unroll
+    for (int k = 0; k < NOUT; k++) dW3[k][r] = 0.f;
 #pragma unroll
   for (int r = 0; r < 16; r++) dB2[r] = 0.f;
-  bf16x8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; j++) ones[j] = __bf16(1.f);
   float db3[NOUT], dls[ACT], st[3] = {0.f, 0.f, 0.f};  // st: pg sum, vf sum, clipped count
 #pragma unroll
   for (int k = 0; k < NOUT; k++) db3[k] = 0.f;
@@ -393,7 +408,13 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       X3 xb;
 #pragma unroll
       for (int p = 0; p < 3; p++) xb.p[p] = rd16(XO, p * XIMG + (32 * t + l32) * XROW + 16 * h);
-      acc = mma3(w1x, xb, acc);
+      {
+        f32x16 sm;
+#pragma unroll
+        for (int r = 0; r < 16; r++) sm[r] = 0.f;
+        mma3s(w1x, xb, acc, sm);
+        acc += sm;
+      }
       if constexpr (DUMP) {
         LP_DUMP(if (valid[t])
           for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 0, 32 * w + acc_row(r, h), acc[r]));
@@ -416,6 +437,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
     for (int r = 0; r < 16; r++) h2[0][r] = Lf[B_B2 / 4 + 32 * w + acc_row(r, h)];
     h2[1] = h2[0];
+    f32x16 h2s[2];
+#pragma unroll
+    for (int r = 0; r < 16; r++) { h2s[0][r] = 0.f; h2s[1][r] = 0.f; }
     {  // software pipeline: step s's MFMAs with step s + 1's reads and step s + 2's weight pieces in flight
       X3 a = wa0, an = wa1, b[2];
 #pragma unroll
@@ -433,13 +457,15 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
             for (int p = 0; p < 3; p++) bn[t].p[p] = rd16(L, B_H1P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
         }
 #pragma unroll
-        for (int t = 0; t < 2; t++) h2[t] = mma3(a, b[t], h2[t]);
+        for (int t = 0; t < 2; t++) mma3s(a, b[t], h2[t], h2s[t]);
         if (s < 6) X3_PIPE_V(3, 6, 12);
         else if (s < 7) X3_PIPE(6, 12);
         X3_SB();
         if (s < 7) { a = an; an = ann; b[0] = bn[0]; b[1] = bn[1]; }
       }
     }
+#pragma unroll
+    for (int t = 0; t < 2; t++) h2[t] += h2s[t];
 #else
     f32x16 h2[2];
     for (int r = 0; r < 16; r++) { h2[0][r] = Lf[r]; h2[1][r] = Lf[r + 16]; }
@@ -521,17 +547,13 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
       if (acc_lane) {
 #pragma unroll
-        for (int k = 0; k < NOUT; k++) {
-          db3[k] += d[t][k];
-          Lf[B_DM / 4 + e * 4 + k] = d[t][k];
-        }
+        for (int k = 0; k < NOUT; k++) db3[k] += d[t][k];
       }
     }
     LP(5);
-    // ---- dh2 (E form) -> DH2 pieces; relu(h2) -> f32 image; db2 per lane
+    // ---- dh2 (E form) -> DH2 pieces; dW3 per lane
 #pragma unroll
     for (int t = 0; t < 2; t++) {
-      float* rowh = Lf + B_H2 / 4 + (32 * t + l32) * SH + 32 * w;
 #pragma unroll
       for (int gg = 0; gg < 4; gg++) {
         float v[4];
@@ -544,16 +566,17 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
           for (int k = 0; k < NOUT; k++) gsum = fmaf(wk[k], d[t][k], gsum);
           v[u] = h2[t][r] > 0.f ? gsum : 0.f;
+#pragma unroll
+          for (int k = 0; k < NOUT; k++) dW3[k][r] = fmaf(d[t][k], h2[t][r], dW3[k][r]);  // h2: relu'd
+          dB2[r] += v[u];
         }
         const X3h x = split4(v);
         const int off = soff(32 * t + l32, 4 * w + gg) + 8 * h;
 #pragma unroll
         for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_DH2P + p * IMG + off) = x.p[p];
-        *reinterpret_cast<float2*>(rowh + 8 * gg + 4 * h) = make_float2(h2[t][4 * gg], h2[t][4 * gg + 1]);
-        *reinterpret_cast<float2*>(rowh + 8 * gg + 4 * h + 2) = make_float2(h2[t][4 * gg + 2], h2[t][4 * gg + 3]);
       }
     }
-    X3_BAR();  // B4: DH2, relu(h2) and dL/dmean images complete
+    X3_BAR();  // B4: DH2 image complete
     const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);  // dh1's first two k-steps: in flight through dW2
     LP(6);
 
@@ -583,13 +606,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
           if (jb < 3) bn = trblk(B_H1P, s, 4 * (jb + 1) + tr_col);
           else if (s < 3) { an = trblk(B_DH2P, s + 1, 4 * w + tr_col); bn = trblk(B_H1P, s + 1, tr_col); }
           dW2[jb] = mma3(a, b, dW2[jb]);
-          if (jb == 0) {  // db2 = sum over the rows of dh2: the three pieces of dW2's A operand times ones
-            dB2 = mfma16(a.p[2], ones, dB2);
-            dB2 = mfma16(a.p[1], ones, dB2);
-            dB2 = mfma16(a.p[0], ones, dB2);
-          }
-          if (jb == 0) X3_PIPE(6, 9);
-          else if (jb < 3) X3_PIPE(6, 6);
+          if (jb < 3) X3_PIPE(6, 6);
           else if (s < 3) X3_PIPE(12, 6);
           X3_SB();
           if (jb < 3) b = bn;
@@ -599,23 +616,13 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     }
 #endif
     LP(7);
-    // ---- dW3 columns 32w.. (f32 16x16x4: A = dL/dmean^T (rows = outputs), B = relu(h2) rows)
-#pragma unroll
-    for (int s = 0; s < 16; s++) {
-      const int e = 4 * s + (lane >> 4), k = lane & 15;
-      const float a = Lf[B_DM / 4 + e * 4 + (k & 3)];  // output rows o >= NOUT are never stored
-#pragma unroll
-      for (int b = 0; b < 2; b++) {
-        const float hv = Lf[B_H2 / 4 + e * SH + 32 * w + 16 * b + k];
-        dW3[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, hv, dW3[b], 0, 0, 0);
-      }
-    }
     LP(8);
 #if !defined(QD_X3_NODH1)
     // ---- dh1 (R form) = relu'(h1) . (dh2 W2[:, block w]); then the dW1 slab (+ db1 in column 12)
     f32x16 dh1[2];
 #pragma unroll
     for (int r = 0; r < 16; r++) { dh1[0][r] = 0.f; dh1[1][r] = 0.f; }
+    f32x16 dh1s[2] = {dh1[0], dh1[1]};
     {  // software pipeline as L2: A = DH2 row reads, B = pre-split W2 columns
       X3 b = wb0, bn = wb1, a[2];
 #pragma unroll
@@ -633,14 +640,31 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
             for (int p = 0; p < 3; p++) an[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
         }
 #pragma unroll
-        for (int t = 0; t < 2; t++) dh1[t] = mma3(a[t], b, dh1[t]);
+        for (int t = 0; t < 2; t++) {
+#if defined(QD_X3_DH1ONE)
+          dh1[t] = mma3(a[t], b, dh1[t]);
+#else
+          mma3s(a[t], b, dh1[t], dh1s[t]);
+#endif
+        }
         if (s < 6) X3_PIPE_V(3, 6, 12);
         else if (s < 7) X3_PIPE(6, 12);
         X3_SB();
         if (s < 7) { b = bn; bn = bnn; a[0] = an[0]; a[1] = an[1]; }
       }
     }
+#pragma unroll
+    for (int t = 0; t < 2; t++) dh1[t] += dh1s[t];
     LP(9);
+    // this round's dW1 in fresh accumulators (big / small terms), added to the launch total with
+    // round-to-nearest VALU adds: one MFMA chain over every row of the block drifted by the
+    // truncation bias (mma3s). The previous round's are added here, a round after their MFMAs
+    // issued (no wait on them). Costs ~2.5 % of the launch (the flush's ~130 AGPR moves and adds
+    // per round; flushing every 4th round under a branch spilled); buys first-layer gradients
+    // within torch fp32's error (tests/test_gpu_learner.py)
+    dW1 += dW1b + dW1s;
+#pragma unroll
+    for (int r = 0; r < 16; r++) { dW1b[r] = 0.f; dW1s[r] = 0.f; }
 #pragma unroll
     for (int t = 0; t < 2; t++) {
       f32x16& acc = dh1[t];
@@ -668,12 +692,13 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
           const int o1 = ghi ? o0 : o0 + 8 * XROW;
           b.p[p] = cat_tr(rdtr(XO, o0), rdtr(XO, o1));
         }
-        dW1 = mma3(a, b, dW1);
+        mma3s(a, b, dW1b, dW1s);
       }
     }
   #endif
     LP(10);
 }
+  dW1 += dW1b + dW1s;
 #if defined(QD_LPROBE)
   if (DUMP && lane == 0) {
     uint64_t* o = reinterpret_cast<uint64_t*>(g.dump) + (size_t(blockIdx.x) * 4 + size_t(w)) * 16;
@@ -692,15 +717,24 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
     for (int j = 0; j < 4; j++) P[P_W2 + n * H + 32 * j + l32] = dW2[j][r];
   }
-  if (lane < 16) {  // rows o < 4 of the 16x16 outputs: lanes 0..15, register o
+  // dW3: sum the per-lane partials over the 32 lanes (rows) of each half; lane 0 of the half holds
+  // neurons 32w + acc_row(r, h)
 #pragma unroll
-    for (int b = 0; b < 2; b++)
+  for (int r = 0; r < 16; r++) {
 #pragma unroll
-      for (int r = 0; r < NOUT; r++) P[P_W3 + r * H + 32 * w + 16 * b + lane] = dW3[b][r];
+    for (int k = 0; k < NOUT; k++) {
+      float x = dW3[k][r];
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      if (l32 == 0) P[P_W3 + k * H + 32 * w + acc_row(r, h)] = x;
+    }
   }
-  if (l32 == 0) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) P[P_B2 + 32 * w + acc_row(r, h)] = dB2[r];
+  for (int r = 0; r < 16; r++) {  // db2: the same lane sum
+    float x = dB2[r];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (l32 == 0) P[P_B2 + 32 * w + acc_row(r, h)] = x;
   }
   if (w == 0) {  // lanes 0..31 hold the per-row sums (lanes 32..63 hold zeros)
     float v[NOUT + ACT + 3];
