@@ -37,7 +37,7 @@ def main():
     for rep in range(3):
         L.grads(obs, act, lp, adv, ret, idx, hidden=hidden)
         torch.cuda.synchronize()
-    st = hidden.view(-1).view(torch.int64)[: 16 * 4 * 4096].view(-1, 16).cpu().numpy()
+    st = hidden.view(-1).view(torch.int64)[: 16 * 8 * 4096].view(-1, 16).cpu().numpy()
     st = st[st[:, 0] != 0]
     for nout, nm in ((4, "actor"), (1, "critic")):
         a = st[st[:, 15] == nout].astype(np.float64)

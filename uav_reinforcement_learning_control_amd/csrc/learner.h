@@ -72,10 +72,60 @@ inline Layout layout_of(int32_t batch, int actor_share) {
   return l;
 }
 
-// the bf16x3 form (learner_x3.hip): its actor share and launcher
-int x3_actor_share();
-int launch_ppo_grad_x3(const GArgs& g, hipStream_t s);  // k_split_w2 + k_ppo_grad_x3
-int launch_ppo_grad_x3_dump(const GArgs& g, hipStream_t s);
+// The bf16x3 form (learner_x3.hip): every block runs both nets over the same rows (the actor's
+// rounds, then the critic's), X3_BLOCKS blocks = one per CU, so every CU carries the same work. A
+// split of the CUs between the nets (the f32 form's actor share) left the slower net's blocks ~5 %
+// longer than the average at any share (round granularity).
+constexpr int X3_BLOCKS = 256;
+inline Layout layout_both(int32_t batch) {
+  Layout l{};
+  const int rounds = (batch + RND - 1) / RND;
+  const int nb = rounds < X3_BLOCKS ? rounds : X3_BLOCKS;
+  l.nb = l.nbc = nb;
+  l.per_block = l.per_block_c = ((rounds + nb - 1) / nb) * RND;
+  l.part_bytes = int64_t(2) * nb * PSTRIDE * int64_t(sizeof(float));
+  l.adv_bytes = int64_t(ADV_BLOCKS) * 2 * int64_t(sizeof(double));
+  l.wimg_bytes = WIMG_BYTES;
+  return l;
+}
+// k_x3_prep (the W2 split, + the advantage statistics when adv_stats != NULL) + k_ppo_grad_x3
+int launch_ppo_grad_x3(const GArgs& g, hipStream_t s, double* adv_stats, const float* adv);
+int launch_ppo_grad_x3_dump(const GArgs& g, hipStream_t s, double* adv_stats, const float* adv);
+
+// Block `blk` of the minibatch advantage statistics (sum and sum of squares in float64; fixed
+// order: per-thread strided over i = blk * 256 + tid + k * ADV_BLOCKS * 256, then a tree) into
+// part[2 blk], part[2 blk + 1]. The index loads and the gathers go out 8 at a time (the sums keep the
+// same order): one at a time, each thread waited out 8 dependent HBM round trips (12.4 us per
+// 524,288-row minibatch under rocprof). Needs 256 threads and `red` [2][256] in LDS.
+__device__ __forceinline__ void adv_stats_block(const float* __restrict__ adv, const int64_t* __restrict__ idx,
+                                                int batch, double* __restrict__ part, int blk, double (*red)[256]) {
+  const int tid = threadIdx.x;
+  double s = 0.0, s2 = 0.0;
+  constexpr int STRIDE = ADV_BLOCKS * 256, U = 8;
+  for (int i0 = blk * 256 + tid; i0 < batch; i0 += U * STRIDE) {
+    int64_t j[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) j[u] = i0 + u * STRIDE < batch ? idx[i0 + u * STRIDE] : int64_t(-1);
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = j[u] >= 0 ? adv[j[u]] : 0.f;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (j[u] < 0) continue;
+      const double d = v[u];
+      s += d;
+      s2 += d * d;
+    }
+  }
+  red[0][tid] = s;
+  red[1][tid] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) { red[0][tid] += red[0][tid + o]; red[1][tid] += red[1][tid + o]; }
+    __syncthreads();
+  }
+  if (tid == 0) { part[2 * blk] = red[0][0]; part[2 * blk + 1] = red[1][0]; }
+}
 
 // Diagnostics (quad_ppo_hidden): the kernels' own hidden pre-activations of minibatch row `pos`
 // (before the ReLU; layer 0 = h1, 1 = h2) -- the dump instantiation of the same body, so the same

@@ -436,24 +436,11 @@ __global__ __launch_bounds__(LB, 1) void k_ppo_grad_dump(GArgs g) {
   else body<1, true>(g, lds_d, blockIdx.x - g.nb);
 }
 
-// minibatch sums of adv and adv^2 in float64 (fixed order: per-thread strided, then a tree)
+// minibatch sums of adv and adv^2 in float64 (adv_stats_block, learner.h)
 __global__ __launch_bounds__(256) void k_adv_stats(const float* __restrict__ adv, const int64_t* __restrict__ idx,
                                                    int batch, double* __restrict__ part) {
   __shared__ double red[2][256];
-  double s = 0.0, s2 = 0.0;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < batch; i += ADV_BLOCKS * 256) {
-    const double v = adv[idx[i]];
-    s += v;
-    s2 += v * v;
-  }
-  red[0][threadIdx.x] = s;
-  red[1][threadIdx.x] = s2;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (int(threadIdx.x) < o) { red[0][threadIdx.x] += red[0][threadIdx.x + o]; red[1][threadIdx.x] += red[1][threadIdx.x + o]; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) { part[2 * blockIdx.x] = red[0][0]; part[2 * blockIdx.x + 1] = red[1][0]; }
+  adv_stats_block(adv, idx, batch, part, blockIdx.x, red);
 }
 
 struct RArgs {
@@ -465,25 +452,37 @@ struct RArgs {
   float inv_batch, ent_coef;
 };
 
-// one thread per (net, parameter): sum of the nb block partials in block order, in float64 (the
-// partials of a bias or head gradient are sums over disjoint row sets that largely cancel)
+// (net, parameter) sums of the nb block partials, in float64 (the partials of a bias or head
+// gradient are sums over disjoint row sets that largely cancel): 64 parameters per block, each
+// summed by 4 threads over consecutive quarters of the blocks (block order within a quarter), the
+// quarters then added in order. One thread per parameter left 147 blocks to stream the 38 MB
+// partial image of the bf16x3 form (13.3 us)
+constexpr int RQ = 4;
 __global__ __launch_bounds__(256) void k_ppo_reduce(RArgs a) {
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= 2 * PSTRIDE) return;
-  const int net = q / PSTRIDE, p = q % PSTRIDE;
+  __shared__ double qs[RQ][64];
+  const int pl = threadIdx.x & 63, qt = threadIdx.x >> 6;
+  const int q = blockIdx.x * 64 + pl;
+  const bool live = q < 2 * PSTRIDE;
+  const int net = live ? q / PSTRIDE : 0, p = live ? q % PSTRIDE : 0;
   const float* src = a.part + size_t(net) * a.nb * PSTRIDE + p;
   const int nb = net ? a.nbc : a.nb;
+  const int per = (nb + RQ - 1) / RQ, b0 = qt * per, b1 = min(nb, b0 + per);
   double sd = 0.0;
-  int b = 0;
-  for (; b + 16 <= nb; b += 16) {  // 16 loads in flight per thread; summed in block order
-    float v[16];
+  int b = b0;
+  if (live) {
+    for (; b + 8 <= b1; b += 8) {  // 8 loads in flight per thread; summed in block order
+      float v[8];
 #pragma unroll
-    for (int u = 0; u < 16; u++) v[u] = src[size_t(b + u) * PSTRIDE];
+      for (int u = 0; u < 8; u++) v[u] = src[size_t(b + u) * PSTRIDE];
 #pragma unroll
-    for (int u = 0; u < 16; u++) sd += double(v[u]);
+      for (int u = 0; u < 8; u++) sd += double(v[u]);
+    }
+    for (; b < b1; b++) sd += double(src[size_t(b) * PSTRIDE]);
   }
-  for (; b < nb; b++) sd += double(src[size_t(b) * PSTRIDE]);
-  const float s = float(sd);
+  qs[qt][pl] = sd;
+  __syncthreads();
+  if (qt != 0 || !live) return;
+  const float s = float(((qs[0][pl] + qs[1][pl]) + qs[2][pl]) + qs[3][pl]);
   const QuadPolicyGrads& g = a.gr;
   if (p < P_B1) { (net ? g.vf_w0 : g.pi_w0)[p - P_W1] = s; return; }
   if (p < P_W2) { (net ? g.vf_b0 : g.pi_b0)[p - P_B1] = s; return; }
@@ -639,7 +638,8 @@ extern "C" {
 int64_t quad_ppo_workspace_bytes(int32_t batch) {
   if (batch < 1) return 0;
   const Layout l = layout_of(batch, ACTOR_SHARE);  // the partial image is sized for every split
-  return l.adv_bytes + l.part_bytes + l.wimg_bytes;
+  const Layout lb = layout_both(batch);             // the bf16x3 form's
+  return l.adv_bytes + (lb.part_bytes > l.part_bytes ? lb.part_bytes : l.part_bytes) + l.wimg_bytes;
 }
 
 // 1: the bf16x3 form (k_ppo_grad_x3, default), 0: the f32-input MFMA form (k_ppo_grad);
@@ -671,7 +671,7 @@ int ppo_grad_impl(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   if (reinterpret_cast<uintptr_t>(workspace) & 15u) return lfail(QUAD_EINVAL, "workspace must be 16-byte aligned");
   if (!(b->clip_range > 0.f)) return lfail(QUAD_EINVAL, "clip_range must be > 0");
   const bool x3 = quad_ppo_grad_form() == 1;
-  const Layout l = layout_of(b->batch, x3 ? x3_actor_share() : ACTOR_SHARE);
+  const Layout l = x3 ? layout_both(b->batch) : layout_of(b->batch, ACTOR_SHARE);
   if (dump && int64_t(b->batch) * 2 * 256 * 4 > (int64_t(1) << 40)) return lfail(QUAD_EINVAL, "batch too large to dump");
   if (workspace_bytes < l.adv_bytes + l.part_bytes + (x3 ? l.wimg_bytes : 0))
     return lfail(QUAD_EINVAL, "workspace too small");
@@ -691,7 +691,8 @@ int ppo_grad_impl(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   double* adv_part = static_cast<double*>(workspace);
   float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) + l.adv_bytes);
   const bool norm = b->normalize_advantage && b->batch > 1;
-  if (norm && b->normalize_advantage != QUAD_ADV_PRECOMPUTED) {  // (2: quad_ppo_adv_stats ran for this batch)
+  const bool need_stats = norm && b->normalize_advantage != QUAD_ADV_PRECOMPUTED;  // (2: quad_ppo_adv_stats ran)
+  if (need_stats && !x3) {  // the bf16x3 form computes them in its prep launch
     hipLaunchKernelGGL(k_adv_stats, dim3(ADV_BLOCKS), dim3(256), 0, s, b->advantages, b->index, b->batch, adv_part);
     if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_adv_stats launch failed");
   }
@@ -708,7 +709,9 @@ int ppo_grad_impl(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   g.dump = dump;
   g.wimg = static_cast<char*>(workspace) + l.adv_bytes + l.part_bytes;
   if (x3) {
-    if (int rc = dump ? launch_ppo_grad_x3_dump(g, s) : launch_ppo_grad_x3(g, s)) return rc;
+    double* st = need_stats ? adv_part : nullptr;
+    if (int rc = dump ? launch_ppo_grad_x3_dump(g, s, st, b->advantages) : launch_ppo_grad_x3(g, s, st, b->advantages))
+      return rc;
   } else if (dump) {
     hipLaunchKernelGGL(k_ppo_grad_dump, dim3(l.nb + l.nbc), dim3(LB), lds_bytes, s, g);
     if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_grad_dump launch failed");
@@ -719,7 +722,7 @@ int ppo_grad_impl(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   RArgs r{};
   r.gr = *gr; r.part = part; r.log_std = p->log_std; r.stats = b->stats; r.nb = l.nb; r.nbc = l.nbc;
   r.inv_batch = 1.0f / float(b->batch); r.ent_coef = b->ent_coef;
-  hipLaunchKernelGGL(k_ppo_reduce, dim3((2 * PSTRIDE + 255) / 256), dim3(256), 0, s, r);
+  hipLaunchKernelGGL(k_ppo_reduce, dim3((2 * PSTRIDE + 63) / 64), dim3(256), 0, s, r);
   if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_ppo_reduce launch failed");
   return QUAD_OK;
 }

@@ -14,7 +14,7 @@
 // Structure (per block: one net, 4 waves, wave w owns neurons 32w..32w+31 of both hidden layers,
 // rounds of 64 minibatch rows = two 32-row tiles; the loss math is learner.hip's):
 //   L1   h1^T = W1 x^T        E form (neurons in registers, rows on lanes)  -> H1 pieces image
-//   L2   h2^T = W2 h1^T       E form: A = W2 rows (pre-split pieces from HBM, k_split_w2), B = H1 row reads
+//   L2   h2^T = W2 h1^T       E form: A = W2 rows (pre-split pieces from HBM, k_x3_prep), B = H1 row reads
 //   head / loss / dL/dmean    VALU, as learner.hip
 //   dh2  E form               -> DH2 pieces image; dW3 += dmean^T relu(h2) per lane (f32 FMAs in
 //        registers, rows = lanes; the 32 lanes of each half are summed once at the end of the launch)
@@ -173,7 +173,7 @@ __device__ __forceinline__ f32x16 mma3(const X3& a, const X3& b, f32x16 c) {
 }
 
 // The W2 fragments a wave multiplies with, as bf16 pieces in HBM (L2-resident, 96 KB per net),
-// split once per launch by k_split_w2: unit (16 bytes) of (net, wave w, use u, k-step s, piece p,
+// split once per launch by k_x3_prep: unit (16 bytes) of (net, wave w, use u, k-step s, piece p,
 // lane). Use 0 = A of L2: W2[n_own][kk]; use 1 = B of dh1: W2[kk][n_own]; kk = 8s + 64h + j for
 // lane half h, element j (n_own = 32w + lane % 32). Loading the pieces (3 dwordx4 per k-step)
 // replaces re-splitting f32 slices held in registers each round (~45 VALU per k-step and operand,
@@ -183,10 +183,13 @@ __device__ __forceinline__ int wimg_unit(int net, int w, int u, int s, int p, in
 }
 static_assert(int64_t(2 * 4 * 2 * 8 * 3 * 64) * 16 == WIMG_BYTES, "pre-split image size");
 
-__global__ __launch_bounds__(64) void k_split_w2(const float* __restrict__ wa, const float* __restrict__ wc,
-                                                 bf16x8* __restrict__ img) {
-  const int b = blockIdx.x, s = b & 7, u = (b >> 3) & 1, w = (b >> 4) & 3, net = b >> 6;
-  const int lane = threadIdx.x, h = lane >> 5, n_own = 32 * w + (lane & 31);
+// k_x3_prep: blocks 0..31 split W2 (four (net, w, u, s) units of 64 lanes per 256-thread block);
+// with adv != NULL blocks 32.. are the advantage-statistics blocks (adv_stats_block) -- one launch
+// for both pre-passes of the gradient kernel
+__device__ __forceinline__ void split_w2_unit(const float* __restrict__ wa, const float* __restrict__ wc,
+                                              bf16x8* __restrict__ img, int b) {
+  const int s = b & 7, u = (b >> 3) & 1, w = (b >> 4) & 3, net = b >> 6;
+  const int lane = threadIdx.x & 63, h = lane >> 5, n_own = 32 * w + (lane & 31);
   const float* w1 = net ? wc : wa;
   float v[8];
 #pragma unroll
@@ -197,6 +200,24 @@ __global__ __launch_bounds__(64) void k_split_w2(const float* __restrict__ wa, c
   const X3 x = split8(v);
 #pragma unroll
   for (int p = 0; p < 3; p++) img[wimg_unit(net, w, u, s, p, lane)] = x.p[p];
+}
+constexpr int SPLIT_BLOCKS = 128 / 4;
+__global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, const float* __restrict__ wc,
+                                                 bf16x8* __restrict__ img, const float* __restrict__ adv,
+                                                 const int64_t* __restrict__ idx, int batch, double* __restrict__ part) {
+  __shared__ double red[2][256];
+  if (int(blockIdx.x) < SPLIT_BLOCKS) {
+    split_w2_unit(wa, wc, img, 4 * blockIdx.x + (threadIdx.x >> 6));
+    return;
+  }
+  adv_stats_block(adv, idx, batch, part, blockIdx.x - SPLIT_BLOCKS, red);
+}
+int launch_prep(const GArgs& g, hipStream_t s, double* adv_stats, const float* adv) {
+  hipLaunchKernelGGL(k_x3_prep, dim3(SPLIT_BLOCKS + (adv_stats ? ADV_BLOCKS : 0)), dim3(256), 0, s, g.actor.w1,
+                     g.critic.w1, const_cast<bf16x8*>(static_cast<const bf16x8*>(g.wimg)), adv, g.idx, g.batch,
+                     adv_stats);
+  if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_x3_prep launch failed");
+  return QUAD_OK;
 }
 
 // the same product with the five small terms in their own accumulator `sm` (magnitude ~2^-8 of the
@@ -294,7 +315,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     for (int j = 0; j < 8; j++) v[j] = 8 * h + j < OBS ? W.w0[n_own * OBS + 8 * h + j] : 0.f;
     w1x = split8(v);
   }
-  // this wave's pre-split W2 fragments (k_split_w2); the base is made opaque each round so the
+  // this wave's pre-split W2 fragments (k_x3_prep); the base is made opaque each round so the
   // compiler cannot hoist the 48 loads out of the round loop (their 192 VGPRs would spill)
   const int wunit0 = wimg_unit(NOUT == ACT ? 0 : 1, w, 0, 0, 0, lane);
   float ls[ACT], sd[ACT], isd[ACT];  // isd: the row loop multiplies (a full-precision division is ~10 VALU)
@@ -701,7 +722,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   dW1 += dW1b + dW1s;
 #if defined(QD_LPROBE)
   if (DUMP && lane == 0) {
-    uint64_t* o = reinterpret_cast<uint64_t*>(g.dump) + (size_t(blockIdx.x) * 4 + size_t(w)) * 16;
+    uint64_t* o = reinterpret_cast<uint64_t*>(g.dump) + (size_t(blockIdx.x) * 8 + (NOUT == ACT ? 0 : 4) + size_t(w)) * 16;
     for (int k = 0; k < 11; k++) o[k] = stp[k];
     o[15] = NOUT;
   }
@@ -766,17 +787,20 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   }
 }
 
+// block b: the actor over its rows, then the critic over the same rows (layout_both)
 __global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3(GArgs g) {
   extern __shared__ __attribute__((aligned(16))) char lds_x3[];
-  if (int(blockIdx.x) < g.nb) body<ACT>(g, lds_x3, blockIdx.x);
-  else body<1>(g, lds_x3, blockIdx.x - g.nb);
+  body<ACT>(g, lds_x3, blockIdx.x);
+  __syncthreads();  // the critic's first writes reuse LDS the actor's last round still reads
+  body<1>(g, lds_x3, blockIdx.x);
 }
 
 // diagnostics: the same body with the hidden pre-activations recorded (quad_ppo_hidden)
 __global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3_dump(GArgs g) {
   extern __shared__ __attribute__((aligned(16))) char lds_x3d[];
-  if (int(blockIdx.x) < g.nb) body<ACT, true>(g, lds_x3d, blockIdx.x);
-  else body<1, true>(g, lds_x3d, blockIdx.x - g.nb);
+  body<ACT, true>(g, lds_x3d, blockIdx.x);
+  __syncthreads();
+  body<1, true>(g, lds_x3d, blockIdx.x);
 }
 
 // one net per kernel (QUADENV_LEARNER_SPLIT=1): each gets its own register allocation; the two
@@ -789,22 +813,7 @@ __global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3_net(GArgs g) {
 
 }  // namespace
 
-#ifndef QD_LRN_X3_ACTOR_SHARE
-// measured (524,288 rows), round 2: 520 -> 0.96 ms, 540 -> 0.94-0.95, 580 -> 0.88-0.89, 600 -> 0.92;
-// round 3 with the pre-split W2 pieces (the actor round dropped 29.8k -> 24.3k cycles, the critic
-// 23.0k -> 22.0k): 500 -> 795 us, 520 -> 782, 540 -> 781, 560 -> 808, 580 -> 829 (old kernel 811)
-#define QD_LRN_X3_ACTOR_SHARE 530
-#endif
-int x3_actor_share() {  // QUADENV_X3_ACTOR_SHARE (per mille, 100..900): A/B sweeps only
-  static const int v = [] {
-    const char* e = std::getenv("QUADENV_X3_ACTOR_SHARE");
-    const int x = e ? std::atoi(e) : 0;
-    return x >= 100 && x <= 900 ? x : QD_LRN_X3_ACTOR_SHARE;
-  }();
-  return v;
-}
-
-int launch_ppo_grad_x3(const GArgs& g, hipStream_t s) {
+int launch_ppo_grad_x3(const GArgs& g, hipStream_t s, double* adv_stats, const float* adv) {
   static bool opted[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return set_error(QUAD_EHIP, "hipGetDevice failed");
@@ -814,9 +823,7 @@ int launch_ppo_grad_x3(const GArgs& g, hipStream_t s) {
       return set_error(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     opted[dev] = true;
   }
-  hipLaunchKernelGGL(k_split_w2, dim3(128), dim3(64), 0, s, g.actor.w1, g.critic.w1,
-                     const_cast<bf16x8*>(static_cast<const bf16x8*>(g.wimg)));
-  if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_split_w2 launch failed");
+  if (int rc = launch_prep(g, s, adv_stats, adv)) return rc;
   const char* sp = std::getenv("QUADENV_LEARNER_SPLIT");
   if (sp && std::atoi(sp) != 0) {
     static hipStream_t s2[64] = {};
@@ -845,19 +852,17 @@ int launch_ppo_grad_x3(const GArgs& g, hipStream_t s) {
       return set_error(QUAD_EHIP, "learner split: join failed");
     return QUAD_OK;
   }
-  hipLaunchKernelGGL(k_ppo_grad_x3, dim3(g.nb + g.nbc), dim3(LB), B_TOTAL, s, g);
+  hipLaunchKernelGGL(k_ppo_grad_x3, dim3(g.nb), dim3(LB), B_TOTAL, s, g);
   if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3 launch failed");
   return QUAD_OK;
 }
 
-int launch_ppo_grad_x3_dump(const GArgs& g, hipStream_t s) {
+int launch_ppo_grad_x3_dump(const GArgs& g, hipStream_t s, double* adv_stats, const float* adv) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_x3_dump), hipFuncAttributeMaxDynamicSharedMemorySize,
                           B_TOTAL) != hipSuccess)
     return set_error(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-  hipLaunchKernelGGL(k_split_w2, dim3(128), dim3(64), 0, s, g.actor.w1, g.critic.w1,
-                     const_cast<bf16x8*>(static_cast<const bf16x8*>(g.wimg)));
-  if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_split_w2 launch failed");
-  hipLaunchKernelGGL(k_ppo_grad_x3_dump, dim3(g.nb + g.nbc), dim3(LB), B_TOTAL, s, g);
+  if (int rc = launch_prep(g, s, adv_stats, adv)) return rc;
+  hipLaunchKernelGGL(k_ppo_grad_x3_dump, dim3(g.nb), dim3(LB), B_TOTAL, s, g);
   if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3_dump launch failed");
   return QUAD_OK;
 }
