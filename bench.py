@@ -323,7 +323,7 @@ def _learner_kernel(m) -> dict:
     flop = 2 * B * (444 * 2048 * 2 * 4 / 64)
     from uav_reinforcement_learning_control_amd import _native as N
     form = int(N.lib().quad_ppo_grad_form())
-    out = {"kernel": "quad_ppo_grad (k_adv_stats + %s + k_ppo_reduce)" % ("k_ppo_grad_x3" if form else "k_ppo_grad"),
+    out = {"kernel": "quad_ppo_grad (%s + k_ppo_reduce)" % ("k_x3_prep + k_ppo_grad_x3" if form else "k_adv_stats + k_ppo_grad"),
            "rows": B, "index_source": "epoch_permutation (quad_permutation), consecutive minibatches",
            "us_per_minibatch": us, "us_per_optimizer_step_device": us_step, "issued_flop": flop}
     if form:
