@@ -78,7 +78,19 @@ __device__ float pack_one(const NetPtrs& p, int nout, int idx) {
 __global__ void k_policy_pack(NetPtrs actor, NetPtrs critic, const float* __restrict__ log_std,
                               float* __restrict__ out) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= PACKED_F) return;
+  if (idx >= PACKED_F + 2 * 32 * 64) return;
+  if (idx >= PACKED_F) {  // one (net, k-step g, lane) unit of the pre-split W2 pieces (policy_net.h)
+    const int u = idx - PACKED_F, net = u / 2048, g = (u / 64) % 32, lane = u % 64;
+    const int f = NET_W2 + (((g & 3) * 4 + (g >> 3)) * 2 + ((g >> 2) & 1)) * 512 + lane * 8;  // w2_frag's
+    float v8[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v8[j] = net ? pack_one(critic, 1, f + j) : pack_one(actor, ACT, f + j);
+    const P3 x = split8(v8);
+    bf16x8* pieces = reinterpret_cast<bf16x8*>(out + PACKED_F);
+#pragma unroll
+    for (int p = 0; p < 3; p++) pieces[((net * 32 + g) * 3 + p) * 64 + lane] = x.p[p];
+    return;
+  }
   float v;
   if (idx < ACTOR_F) v = pack_one(actor, ACT, idx);
   else if (idx < LDS_F) v = pack_one(critic, 1, idx - ACTOR_F);
@@ -131,7 +143,7 @@ __device__ __forceinline__ void load_tile(TileIn& in, const float* __restrict__ 
 // finish step t-1 for one tile: TimeLimit bootstrap r += gamma V(terminal_obs) where truncated and
 // not terminated (critic only when the tile holds such an env), reward row, last_start, episode
 // statistics (accumulated in st[3] of the h == 0 lanes). Returns the env's new last_start.
-__device__ __forceinline__ float epilogue_tile(const float* __restrict__ Lc, const EpiArgs& e,
+__device__ __forceinline__ float epilogue_tile(const float* __restrict__ Lc, const float* packed, const EpiArgs& e,
                                                const TileIn& in, int env, bool ok, size_t row, float st[3]) {
   const int h = (threadIdx.x & 63) >> 5;
   const bool term = in.flags & 1u, trunc = in.flags & 2u;
@@ -140,7 +152,7 @@ __device__ __forceinline__ float epilogue_tile(const float* __restrict__ Lc, con
   if (__any(timeout)) {
     float xb[1][8], v[1][1];
     load_xb(e.terminal_obs, env, ok, xb[0]);
-    net_forward<1, 1>(Lc, xb, v);
+    net_forward<1, 1>(Lc, packed, xb, v);
     tv = v[0][0];
   }
   const bool done = term || trunc;
@@ -250,13 +262,13 @@ __global__ __launch_bounds__(BLK) void k_policy_act(const float* __restrict__ pa
       envs[j] = (g * NT_ACT + j) * TILE + (lane & 31);
       oks[j] = envs[j] < a.n;
       ls[j] = 0.f;
-      if (pend) ls[j] = epilogue_tile(lds + ACTOR_F, e, cur[j], envs[j], oks[j], rowp, st);
+      if (pend) ls[j] = epilogue_tile(lds + ACTOR_F, packed, e, cur[j], envs[j], oks[j], rowp, st);
       else if (a.last_start && oks[j]) ls[j] = a.last_start[envs[j]];
 #pragma unroll
       for (int k = 0; k < 8; k++) xb[j][k] = cur[j].xb[k];
     }
     float mean[NT_ACT][ACT], val[NT_ACT][1];
-    net_forward2<NT_ACT>(lds, xb, mean, val);
+    net_forward2<NT_ACT>(lds, packed, xb, mean, val);
 #pragma unroll
     for (int j = 0; j < NT_ACT; j++) {
       const int env = envs[j];
@@ -307,7 +319,7 @@ __global__ __launch_bounds__(PBLOCK) void k_rollout_post(const float* __restrict
     const int env = tile * TILE + (lane & 31);
     TileIn in;
     load_tile(in, e.terminal_obs, e, true, env, env < n);  // xb unused here
-    epilogue_tile(lds + ACTOR_F, e, in, env, env < n, rowp, st);
+    epilogue_tile(lds + ACTOR_F, packed, e, in, env, env < n, rowp, st);
   }
   flush_stats<PBLOCK>(e.stats, st);
   cursor_arrive(cursor, 0u, 0u, false);
@@ -362,7 +374,7 @@ int check_epi(const QuadRolloutPost* p) {
 
 extern "C" {
 
-int32_t quad_policy_packed_floats(void) { return PACKED_F; }
+int32_t quad_policy_packed_floats(void) { return PACKED_ALL_F; }
 
 int quad_policy_pack(const QuadPolicyParams* p, float* packed, void* stream) {
   if (!p || !packed) return pfail(QUAD_EINVAL, "params/packed is NULL");
@@ -373,7 +385,7 @@ int quad_policy_pack(const QuadPolicyParams* p, float* packed, void* stream) {
   if (int rc = lds_opt_in()) return rc;
   NetPtrs actor{p->pi_w0, p->pi_b0, p->pi_w1, p->pi_b1, p->act_w, p->act_b};
   NetPtrs critic{p->vf_w0, p->vf_b0, p->vf_w1, p->vf_b1, p->val_w, p->val_b};
-  hipLaunchKernelGGL(k_policy_pack, dim3((PACKED_F + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(k_policy_pack, dim3((PACKED_F + 2 * 32 * 64 + 255) / 256), dim3(256), 0,
                      static_cast<hipStream_t>(stream), actor, critic, p->log_std, packed);
   return hipGetLastError() == hipSuccess ? QUAD_OK : pfail(QUAD_EHIP, "k_policy_pack launch failed");
 }

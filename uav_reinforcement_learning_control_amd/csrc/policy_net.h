@@ -45,6 +45,12 @@ constexpr int CRITIC_F = NET_W3 + 128 + 4;
 constexpr int LDS_F = ACTOR_F + CRITIC_F;  // 38,024 floats = 152 KB
 constexpr int PACKED_F = LDS_F + 4;        // + log_std[4]
 static_assert(ACTOR_F % 4 == 0 && LDS_F % 4 == 0, "float4 staging");
+// then the W2 fragments pre-split into three bf16 pieces (k_policy_pack), read from HBM / L2 by
+// the MLP pipeline instead of splitting the f32 fragments from LDS at every step:
+// [net][k-step g 0..31][piece 0..2][lane 0..63] x 16 bytes = 96 KB per net
+constexpr int PIECES_F = 2 * 32 * 3 * 64 * 4;
+constexpr int PACKED_ALL_F = PACKED_F + PIECES_F;
+static_assert(PACKED_F % 4 == 0, "16-byte aligned pieces");
 
 __host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -158,14 +164,28 @@ __device__ __forceinline__ P3 ld_split8(const float* L, int off) {
 #ifndef QD_NF_VPG
 #define QD_NF_VPG 5
 #endif
+typedef __attribute__((address_space(1))) const bf16x8 gbf16x8;  // global loads, not flat
 struct NetOff {
   int w1, w2, b, w3;
+  gbf16x8* wp;  // this net's pre-split W2 pieces, this lane's unit
 };
-__device__ __forceinline__ NetOff net_off(int base) {
+// `packed`: the global packed image; its scalar base is made opaque per call, so the compiler
+// cannot hoist the pieces' loads out of the callers' step loops (hundreds of VGPRs)
+__device__ __forceinline__ NetOff net_off(int base, const float* packed, int net) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
-  NetOff o{base + NET_W1 + lane * 8, base + NET_W2 + lane * 8, base + NET_B1 + h * 16, base + NET_W3 + h * 4};
+  uint64_t pb = reinterpret_cast<uint64_t>(packed + PACKED_F);
+  asm volatile("" : "+s"(pb));
+  NetOff o{base + NET_W1 + lane * 8, base + NET_W2 + lane * 8, base + NET_B1 + h * 16, base + NET_W3 + h * 4,
+           reinterpret_cast<gbf16x8*>(pb) + net * (32 * 3 * 64) + lane};
   asm volatile("" : "+v"(o.w1), "+v"(o.w2), "+v"(o.b), "+v"(o.w3));
   return o;
+}
+// the pre-split W2 fragment of layer-2 k-step g (three dwordx4 loads)
+__device__ __forceinline__ P3 w2_pieces(const NetOff& o, int g) {
+  P3 x;
+#pragma unroll
+  for (int p = 0; p < 3; p++) x.p[p] = o.wp[(g * 3 + p) * 64];
+  return x;
 }
 // W2 fragment of layer-2 k-step g = 8n + 4t + m
 __device__ __forceinline__ int w2_frag(const NetOff& o, int g) {
@@ -197,8 +217,8 @@ __device__ __forceinline__ void split_pair(float x0, float x1, Q3& o, int k) {
 template <int NT>
 struct Pipe {
   Q3 h1[2][NT][2];   // relu(h1) pieces: block n in buffer n & 1 (block 0 of the next net: buffer 0)
-  float4 raw[2][2];  // W2 fragments read ahead (ring of two steps)
-  P3 w;              // the current step's W2 split
+  P3 wr[3];          // pre-split W2 fragments: ring over the global step count (net 32 + g) % 3,
+                     // step g's loaded two steps ahead
 };
 
 // block 0 of a net before its pipeline starts (the first net of a call)
@@ -217,17 +237,14 @@ __device__ __forceinline__ void pipe_start(const float* __restrict__ L, const Ne
       for (int k = 0; k < 4; k++)
         split_pair(relu(a1[8 * t + 2 * k]), relu(a1[8 * t + 2 * k + 1]), st.h1[0][j][t], k);
   }
-  st.raw[0][0] = ld4(L, w2_frag(o, 0)); st.raw[0][1] = ld4(L, w2_frag(o, 0) + 4);
-  st.raw[1][0] = ld4(L, w2_frag(o, 1)); st.raw[1][1] = ld4(L, w2_frag(o, 1) + 4);
-  const float v[8] = {st.raw[0][0].x, st.raw[0][0].y, st.raw[0][0].z, st.raw[0][0].w,
-                      st.raw[0][1].x, st.raw[0][1].y, st.raw[0][1].z, st.raw[0][1].w};
-  st.w = split8(v);
+  st.wr[0] = w2_pieces(o, 0);
+  st.wr[1] = w2_pieces(o, 1);
   __builtin_amdgcn_sched_barrier(0);
 }
 
 // one net's 32 layer-2 steps (+ layer 1 of its blocks 1..3, and with NEXT the next net's block 0
 // and first fragments), then its head
-template <int NOUT, int NT, bool NEXT>
+template <int NOUT, int NT, bool NEXT, int G0>
 __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetOff& o, const NetOff& on,
                                          const P3 (&xp)[NT], Pipe<NT>& st, float (&out)[NT][NOUT]) {
   const int h = (threadIdx.x >> 5) & 1;
@@ -249,22 +266,13 @@ __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetO
 #pragma unroll
     for (int s = 0; s < 8; s++) {
       const int g = 8 * n + s, t = s >> 2, m = s & 3;
-      if (g + 2 < 32 || NEXT) {  // read step g + 2's fragment into the slot step g's split just freed
-        const int f = g + 2 < 32 ? w2_frag(o, g + 2) : w2_frag(on, g + 2 - 32);
-        st.raw[g & 1][0] = ld4(L, f);
-        st.raw[g & 1][1] = ld4(L, f + 4);
-      }
+      if (g + 2 < 32 || NEXT)  // step g + 2's pieces into the ring slot step g - 1 freed
+        st.wr[(G0 + g + 2) % 3] = g + 2 < 32 ? w2_pieces(o, g + 2) : w2_pieces(on, g + 2 - 32);
 #pragma unroll
-      for (int j = 0; j < NT; j++) acc[m][j] = mfma6(st.w, st.h1[cb][j][t].p(), acc[m][j]);
+      for (int j = 0; j < NT; j++) acc[m][j] = mfma6(st.wr[(G0 + g) % 3], st.h1[cb][j][t].p(), acc[m][j]);
       if (pre && s == 1) {
 #pragma unroll
         for (int j = 0; j < NT; j++) a1n[j] = mfma6(w1n, xp[j], b1n);
-      }
-      P3 wn;
-      if (g + 1 < 32 || NEXT) {
-        const float4 r0 = st.raw[(g + 1) & 1][0], r1 = st.raw[(g + 1) & 1][1];
-        const float v[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-        wn = split8(v);
       }
       if (pre && s == 0) {
         bias_init(b1n, L, ol.b + nn * 32);
@@ -286,7 +294,6 @@ __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetO
       }
 #endif
       __builtin_amdgcn_sched_barrier(0);
-      if (g + 1 < 32 || NEXT) st.w = wn;
     }
   }
   float part[NT][NOUT];
@@ -312,30 +319,30 @@ __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetO
 
 // one net (image at L): NOUT = ACT for the actor, 1 for the critic
 template <int NOUT, int NT>
-__device__ __forceinline__ void net_forward(const float* __restrict__ L, const float (&xq)[NT][8],
+__device__ __forceinline__ void net_forward(const float* __restrict__ L, const float* packed, const float (&xq)[NT][8],
                                             float (&out)[NT][NOUT]) {
   P3 xp[NT];
 #pragma unroll
   for (int j = 0; j < NT; j++) xp[j] = split8(xq[j]);
-  const NetOff o = net_off(0);
+  const NetOff o = net_off(0, packed, NOUT == ACT ? 0 : 1);
   Pipe<NT> st;
   pipe_start<NT>(L, o, xp, st);
-  net_core<NOUT, NT, false>(L, o, o, xp, st, out);
+  net_core<NOUT, NT, false, 0>(L, o, o, xp, st, out);
 }
 
 // actor (image at L) then critic (at L + ACTOR_F) in one pipeline: the same bits as two net_forward
 // calls (every tile's operations and their order are the same)
 template <int NT>
-__device__ __forceinline__ void net_forward2(const float* __restrict__ L, const float (&xq)[NT][8],
+__device__ __forceinline__ void net_forward2(const float* __restrict__ L, const float* packed, const float (&xq)[NT][8],
                                              float (&mean)[NT][ACT], float (&val)[NT][1]) {
   P3 xp[NT];
 #pragma unroll
   for (int j = 0; j < NT; j++) xp[j] = split8(xq[j]);
-  const NetOff oa = net_off(0), oc = net_off(ACTOR_F);
+  const NetOff oa = net_off(0, packed, 0), oc = net_off(ACTOR_F, packed, 1);
   Pipe<NT> st;
   pipe_start<NT>(L, oa, xp, st);
-  net_core<ACT, NT, true>(L, oa, oc, xp, st, mean);
-  net_core<1, NT, false>(L, oc, oc, xp, st, val);
+  net_core<ACT, NT, true, 0>(L, oa, oc, xp, st, mean);
+  net_core<1, NT, false, 32>(L, oc, oc, xp, st, val);
 }
 
 // 152 KB global -> LDS per block: batches of 13 float4 loads in flight per thread (a serial

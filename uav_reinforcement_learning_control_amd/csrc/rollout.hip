@@ -160,11 +160,11 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
     }
 #else
 #if defined(QD_ROLL_NOCRITIC)
-    net_forward<ACT, NT>(lds, xb, mean);
+    net_forward<ACT, NT>(lds, packed, xb, mean);
 #pragma unroll
     for (int j = 0; j < NT; j++) val[j][0] = mean[j][0];
 #else
-    net_forward2<NT>(lds, xb, mean, val);
+    net_forward2<NT>(lds, packed, xb, mean, val);
 #endif
 #endif
     float z[ACT] = {0.f, 0.f, 0.f, 0.f};
@@ -201,7 +201,7 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
     if (__any(timeout)) {
       float xt[NT][8], vt[NT][1];
       fragments<NT>(r.obs, xt);
-      net_forward<1, NT>(lds + ACTOR_F, xt, vt);
+      net_forward<1, NT>(lds + ACTOR_F, packed, xt, vt);
       tv = (NT == 2 && h) ? vt[NT - 1][0] : vt[0][0];
     }
     // ---- reward row, Monitor statistics, episode_starts of the next step
