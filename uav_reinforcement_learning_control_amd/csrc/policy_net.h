@@ -345,11 +345,19 @@ __device__ __forceinline__ void net_forward2(const float* __restrict__ L, const 
   net_core<1, NT, false, 32>(L, oc, oc, xp, st, val);
 }
 
-// 152 KB global -> LDS per block: batches of 13 float4 loads in flight per thread (a serial
-// load -> store loop would pay ~38 round trips of L2/MALL latency)
+// the packed image global -> LDS per block, without the two f32 W2 regions (the MLP reads the
+// pre-split pieces from L2 instead): 21 KB of the 152 KB image, in batches of float4 loads in flight
+// per thread (a serial load -> store loop would pay a round trip of L2/MALL latency per float4).
+// Compact float4 index k -> image float4 index: [0, NET_W2) | [NET_B1, ACTOR_F + NET_W2) |
+// [ACTOR_F + NET_B1, LDS_F)
+constexpr int STAGE_V = (LDS_F - 2 * W2_F) / 4;
+__device__ __forceinline__ int stage_map(int k) {
+  constexpr int A = NET_W2 / 4, B = (ACTOR_F + NET_W2 - NET_B1) / 4 + A;
+  return k < A ? k : (k < B ? k + W2_F / 4 : k + W2_F / 2);
+}
 template <int BLK>
 __device__ __forceinline__ void stage_lds(float* lds, const float* __restrict__ packed) {
-  constexpr int NV = LDS_F / 4, PER = (NV + BLK - 1) / BLK, BATCH = BLK >= 512 ? 10 : 13;
+  constexpr int NV = STAGE_V, PER = (NV + BLK - 1) / BLK, BATCH = PER < 8 ? PER : 8;
   const float4* src = reinterpret_cast<const float4*>(packed);
   float4* dst = reinterpret_cast<float4*>(lds);
 #pragma unroll
@@ -358,12 +366,12 @@ __device__ __forceinline__ void stage_lds(float* lds, const float* __restrict__ 
 #pragma unroll
     for (int j = 0; j < BATCH; j++) {
       const int k = (b0 + j) * BLK + threadIdx.x;
-      v[j] = src[k < NV ? k : NV - 1];  // clamped: every element defined, stays in VGPRs
+      v[j] = src[stage_map(k < NV ? k : NV - 1)];  // clamped: every element defined, stays in VGPRs
     }
 #pragma unroll
     for (int j = 0; j < BATCH; j++) {
       const int k = (b0 + j) * BLK + threadIdx.x;
-      if (b0 + j < PER && k < NV) dst[k] = v[j];
+      if (b0 + j < PER && k < NV) dst[stage_map(k)] = v[j];
     }
   }
   __syncthreads();
