@@ -6,9 +6,11 @@
 // what the previous pieces leave (exact), and a product a*b as the six MFMAs a2b0 + a1b1 + a0b2 +
 // a1b0 + a0b1 + a0b0 accumulated in f32; the dropped a1b2 + a2b1 + a2b2 are <= ~2^-23 |ab|. One
 // 16-deep k-step costs 6 x 32 matrix cycles instead of 8 x 64 with v_mfma_f32_32x32x2_f32 (2.7x
-// less). The activations (X^T, relu(h1)^T) are split once per layer; the weights are staged in LDS
-// as f32 (both nets' three-piece W2 would be 192 KB against 160) and split at use, each split
-// shared by the NT tiles of the wave.
+// less). The activations (X^T, relu(h1)^T) are split once per layer. W2 is pre-split once per
+// policy update (k_policy_pack appends the pieces to the packed image, 96 KB per net) and read from
+// L2 two k-steps ahead; W1, biases and head weights are staged in LDS as f32 (21 KB; W1 split at
+// use). Until round 3 the f32 W2 sat in LDS too (both nets' three-piece W2 would be 192 KB against
+// 160) and was split at every step: ~45 VALU per k-step against 12 MFMAs.
 #pragma once
 
 #include <hip/hip_runtime.h>
