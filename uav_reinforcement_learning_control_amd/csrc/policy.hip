@@ -78,7 +78,19 @@ __device__ float pack_one(const NetPtrs& p, int nout, int idx) {
 __global__ void k_policy_pack(NetPtrs actor, NetPtrs critic, const float* __restrict__ log_std,
                               float* __restrict__ out) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= PACKED_F + 2 * 32 * 64) return;
+  if (idx >= PACKED_F + 2 * 32 * 64 + 2 * 4 * 64) return;
+  if (idx >= PACKED_F + 2 * 32 * 64) {  // one (net, layer-1 block n, lane) unit of the W1 pieces
+    const int u = idx - PACKED_F - 2 * 32 * 64, net = u / 256, n = (u / 64) % 4, lane = u % 64;
+    const int f = NET_W1 + n * 512 + lane * 8;
+    float v8[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) v8[j] = net ? pack_one(critic, 1, f + j) : pack_one(actor, ACT, f + j);
+    const P3 x = split8(v8);
+    bf16x8* pieces = reinterpret_cast<bf16x8*>(out + PACKED_F + PIECES_F);
+#pragma unroll
+    for (int p = 0; p < 3; p++) pieces[((net * 4 + n) * 3 + p) * 64 + lane] = x.p[p];
+    return;
+  }
   if (idx >= PACKED_F) {  // one (net, k-step g, lane) unit of the pre-split W2 pieces (policy_net.h)
     const int u = idx - PACKED_F, net = u / 2048, g = (u / 64) % 32, lane = u % 64;
     const int f = NET_W2 + (((g & 3) * 4 + (g >> 3)) * 2 + ((g >> 2) & 1)) * 512 + lane * 8;  // w2_frag's
@@ -385,7 +397,7 @@ int quad_policy_pack(const QuadPolicyParams* p, float* packed, void* stream) {
   if (int rc = lds_opt_in()) return rc;
   NetPtrs actor{p->pi_w0, p->pi_b0, p->pi_w1, p->pi_b1, p->act_w, p->act_b};
   NetPtrs critic{p->vf_w0, p->vf_b0, p->vf_w1, p->vf_b1, p->val_w, p->val_b};
-  hipLaunchKernelGGL(k_policy_pack, dim3((PACKED_F + 2 * 32 * 64 + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(k_policy_pack, dim3((PACKED_F + 2 * 32 * 64 + 2 * 4 * 64 + 255) / 256), dim3(256), 0,
                      static_cast<hipStream_t>(stream), actor, critic, p->log_std, packed);
   return hipGetLastError() == hipSuccess ? QUAD_OK : pfail(QUAD_EHIP, "k_policy_pack launch failed");
 }

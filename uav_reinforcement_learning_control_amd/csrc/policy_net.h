@@ -51,7 +51,9 @@ static_assert(ACTOR_F % 4 == 0 && LDS_F % 4 == 0, "float4 staging");
 // the MLP pipeline instead of splitting the f32 fragments from LDS at every step:
 // [net][k-step g 0..31][piece 0..2][lane 0..63] x 16 bytes = 96 KB per net
 constexpr int PIECES_F = 2 * 32 * 3 * 64 * 4;
-constexpr int PACKED_ALL_F = PACKED_F + PIECES_F;
+// then W1 the same way: [net][block n 0..3][piece][lane] x 16 bytes = 12 KB per net
+constexpr int W1PIECES_F = 2 * 4 * 3 * 64 * 4;
+constexpr int PACKED_ALL_F = PACKED_F + PIECES_F + W1PIECES_F;
 static_assert(PACKED_F % 4 == 0, "16-byte aligned pieces");
 
 __host__ __device__ constexpr int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
@@ -169,7 +171,8 @@ __device__ __forceinline__ P3 ld_split8(const float* L, int off) {
 typedef __attribute__((address_space(1))) const bf16x8 gbf16x8;  // global loads, not flat
 struct NetOff {
   int w1, w2, b, w3;
-  gbf16x8* wp;  // this net's pre-split W2 pieces, this lane's unit
+  gbf16x8* wp;   // this net's pre-split W2 pieces, this lane's unit
+  gbf16x8* w1p;  // and W1's
 };
 // `packed`: the global packed image; its scalar base is made opaque per call, so the compiler
 // cannot hoist the pieces' loads out of the callers' step loops (hundreds of VGPRs)
@@ -178,9 +181,18 @@ __device__ __forceinline__ NetOff net_off(int base, const float* packed, int net
   uint64_t pb = reinterpret_cast<uint64_t>(packed + PACKED_F);
   asm volatile("" : "+s"(pb));
   NetOff o{base + NET_W1 + lane * 8, base + NET_W2 + lane * 8, base + NET_B1 + h * 16, base + NET_W3 + h * 4,
-           reinterpret_cast<gbf16x8*>(pb) + net * (32 * 3 * 64) + lane};
+           reinterpret_cast<gbf16x8*>(pb) + net * (32 * 3 * 64) + lane,
+           reinterpret_cast<gbf16x8*>(pb) + 2 * (32 * 3 * 64) + net * (4 * 3 * 64) + lane};
   asm volatile("" : "+v"(o.w1), "+v"(o.w2), "+v"(o.b), "+v"(o.w3));
   return o;
+}
+// the pre-split W1 fragment of layer-1 block n (k_policy_pack; the same pieces as ld_split8 of the
+// LDS f32, which the four waves of a block would each redo per step)
+__device__ __forceinline__ P3 w1_pieces(const NetOff& o, int n) {
+  P3 x;
+#pragma unroll
+  for (int p = 0; p < 3; p++) x.p[p] = o.w1p[(n * 3 + p) * 64];
+  return x;
 }
 // the pre-split W2 fragment of layer-2 k-step g (three dwordx4 loads)
 __device__ __forceinline__ P3 w2_pieces(const NetOff& o, int g) {
@@ -229,7 +241,7 @@ __device__ __forceinline__ void pipe_start(const float* __restrict__ L, const Ne
                                            Pipe<NT>& st) {
   f32x16 b;
   bias_init(b, L, o.b);
-  const P3 w1 = ld_split8(L, o.w1);
+  const P3 w1 = w1_pieces(o, 0);
 #pragma unroll
   for (int j = 0; j < NT; j++) {
     const f32x16 a1 = mfma6(w1, xp[j], b);
@@ -278,7 +290,7 @@ __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetO
       }
       if (pre && s == 0) {
         bias_init(b1n, L, ol.b + nn * 32);
-        w1n = ld_split8(L, ol.w1 + nn * 512);
+        w1n = w1_pieces(ol, nn);
       }
       if (pre && s >= 2) {  // pair-chunks c = 0..15 (tile c >> 3, half (c >> 2) & 1, pair c & 3) over s = 2..7
 #pragma unroll
