@@ -105,15 +105,15 @@ def _kernel_name(env) -> str:
 
 def _kernel_symbol(env) -> str:
     """The launched hover step kernel's template symbol as rocprofv3 names it (csrc/quadenv.hip
-    quad_step_range: k_step_h<KIND, CTBR, SPEC, HB> with HB = 64 up to 32,768 envs, else 256;
-    k_step<KIND, CTBR, SPEC>; k_step_g<KIND, CTBR, G, SPEC>)."""
+    quad_step_range: k_step_h<KIND, CTBR, SPEC, HB> with HB from quad_kernel_form bit 7 (256-env
+    blocks above 32,768 envs, else 64); k_step<KIND, CTBR, SPEC>; k_step_g<KIND, CTBR, G, SPEC>)."""
     from uav_reinforcement_learning_control_amd import _native as N
     form = int(N.lib().quad_kernel_form(env._h))
     lanes, spec = form & 15, "true" if form & 16 else "false"
     if lanes:
         return f"k_step_g<0, false, {lanes}, {spec}>"
     if form & 32:
-        return f"k_step_h<0, false, {spec}, {64 if env.num_envs <= 32768 else 256}>"
+        return f"k_step_h<0, false, {spec}, {256 if form & 128 else 64}>"
     return f"k_step<0, false, {spec}>"
 
 
@@ -182,22 +182,37 @@ def _run_rank(args, rank, world, local_rank):
             "hover_65536_one_launch_random": _kstep_rate(65536, 200, dev, args.seed),
             "config5_traj_ctbr_65536": _kernel_rate(65536, "trajectory", "RateControlWrapper", dev, args.seed),
             "hover_ctbr_65536": _kernel_rate(65536, "hover", "RateControlWrapper", dev, args.seed)}
-    if rank == 0 and args.large_envs > 0:
-        del actions, g
-        env.close()
+    del actions, g
+    env.close()
+    if rank == 0:
         torch.cuda.empty_cache()
-        big = QuadVecEnv(args.large_envs, env="hover", device=dev, seed=args.seed)
-        big.reset()
-        acts = [big.random_actions(k) for k in range(8)]
-        st = _quad_step_fn(big)
-        for k in range(50):  # past the post-reset transient: ~11 % of envs reset per step from here on
-            st(acts[k % 8].data_ptr())
-        res["large_kernel_us"] = _gated_kernel_us(st, acts, 200)
-        res["large_symbol"] = _kernel_symbol(big)
-        big.close()
-    else:
-        env.close()
+        if args.large_envs > 0:  # Infinity-Cache-assisted (~290 MB working set)
+            res["large"] = _large_point(args.large_envs, dev, args.seed, 200)
+        if args.dram_envs > 0:  # true HBM: 1.2 GB per launch, 4.5x the 256 MB Infinity Cache
+            res["dram"] = _large_point(args.dram_envs, dev, args.seed, 40)
     return res
+
+
+def _large_point(n, dev, seed, launches) -> dict:
+    """The same step at a large batch (the size's default kernel form) after 50 steps (the
+    post-reset transient: ~11 % of envs reset per step from there on): gated per-launch time,
+    HBM roofline of the algorithmic bytes, and the committed PMC traffic of that kernel and size."""
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    big = QuadVecEnv(n, env="hover", device=dev, seed=seed)
+    big.reset()
+    acts = [big.random_actions(k) for k in range(8)]
+    st = _quad_step_fn(big)
+    for k in range(50):
+        st(acts[k % 8].data_ptr())
+    us = _gated_kernel_us(st, acts, launches)
+    sym = _kernel_symbol(big)
+    big.close()
+    del acts
+    torch.cuda.empty_cache()
+    gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
+    return {"envs": n, "kernel_us": us, "env_steps_per_s_kernel": n / (us * 1e-6), "achieved_GBs": gbs,
+            "frac": gbs / HBM_PEAK_GBS, "kernel_symbol": sym, "traffic_pmc": _pmc_traffic(sym, n),
+            "issue": _pmc_issue(sym, n)}
 
 
 def _kernel_rate(n, kind, wrapper, dev, seed) -> dict:
@@ -567,14 +582,20 @@ def _pmc_traffic(symbol: str, n_envs: int):
         return None
 
 
-def _pmc_issue(n_envs: int):
-    """The step kernel's counted issue roofline (rocprofv3 PMC: SQ_INSTS_VALU/SALU, SQ_BUSY_CYCLES,
-    GRBM_GUI_ACTIVE per launch) from the committed summary, if present (tools/pmc/issue_roofline.py)."""
+def _pmc_issue(symbol: str, n_envs: int):
+    """The timed kernel's counted issue roofline (rocprofv3 PMC: instruction counts by class,
+    SQ_WAVE_CYCLES / SQ_BUSY_CYCLES / wait shares, GRBM_GUI_ACTIVE per launch) from the committed
+    summary (tools/pmc/issue_roofline.py -> profiles/pmc_issue.json, keyed by kernel symbol and env
+    count, like the traffic file), or None when no pass of the kernel the bench timed exists."""
     path = os.path.join(REPO, "profiles", "pmc_issue.json")
     if not os.path.exists(path):
         return None
     try:
-        return json.load(open(path)).get(str(n_envs))
+        d = json.load(open(path))
+        rec = d.get("kernels", {}).get(symbol, {}).get(str(n_envs))
+        if not rec:
+            return None
+        return dict(rec, kernel=symbol, envs=n_envs, round=d.get("round"), source="profiles/pmc_issue.json")
     except Exception:
         return None
 
@@ -637,6 +658,7 @@ def main():
     ap.add_argument("--action-batches", type=int, default=256)
     ap.add_argument("--kernel-launches", type=int, default=200)
     ap.add_argument("--large-envs", type=int, default=1 << 20)
+    ap.add_argument("--dram-envs", type=int, default=1 << 22)
     ap.add_argument("--cpu-seconds", type=float, default=7.0)
     ap.add_argument("--rollout-steps", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -701,7 +723,7 @@ def main():
                      "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_pmc": traffic,
                      "kernel": res["kernel"], "kernel_symbol": res["symbol"], "kernel_us": kus,
                      "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs,
-                     "issue": _pmc_issue(args.envs)},
+                     "issue": _pmc_issue(res["symbol"], args.envs)},
     }
     if "rollout" in res:
         line["rollout_phase"] = res["rollout"]
@@ -709,14 +731,11 @@ def main():
         line["end_to_end"] = res["end_to_end"]
     if "configs" in res:
         line["configs"] = res["configs"]
-    if "large_kernel_us" in res:
-        lk = res["large_kernel_us"]
-        line["large_batch"] = {"envs": args.large_envs, "kernel_us": lk,
-                               "env_steps_per_s_kernel": args.large_envs / (lk * 1e-6),
-                               "achieved_GBs": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9,
-                               "frac": BYTES_PER_ENV_STEP * args.large_envs / (lk * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                               "kernel_symbol": res["large_symbol"],
-                               "traffic_pmc": _pmc_traffic(res["large_symbol"], args.large_envs)}
+    if "large" in res:
+        line["large_batch"] = dict(res["large"], note="working set ~290 MB: Infinity-Cache assisted, not a DRAM figure")
+    if "dram" in res:
+        line["large_batch_dram"] = dict(res["dram"], note="1.2 GB per launch (4.5x the 256 MB Infinity Cache): "
+                                                          "the step's true HBM roofline point")
     if not args.no_cpu_baseline and world == 1:
         cores = _cpu_info()["usable_cores"]
         line["cpu_host"] = _cpu_info()

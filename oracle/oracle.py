@@ -116,6 +116,10 @@ def lib():
                                            C.POINTER(C.c_uint32)]
         L.oracle_reset_draw.argtypes = [C.POINTER(OracleCfg), C.c_uint64, C.c_uint64, C.c_uint32,
                                         fp, fp]
+        L.oracle_reset_draw_batch.argtypes = [C.POINTER(OracleCfg), C.c_uint64, C.c_void_p, C.c_void_p,
+                                              C.c_int32, fp, fp]
+        L.oracle_env_reset_batch.argtypes = [C.POINTER(OracleCfg), C.POINTER(OracleEnv), C.c_int32, fp, fp, fp]
+        L.oracle_env_prepare_batch.argtypes = [C.POINTER(OracleCfg), C.POINTER(OracleEnv), C.c_int32]
         L.oracle_random_action.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, fp]
         L.oracle_bench_rollout.argtypes = [C.POINTER(OracleCfg), C.c_int32, C.c_int32, C.c_uint64]
         L.oracle_bench_rollout.restype = C.c_double
@@ -206,6 +210,66 @@ def reset_draw(cfg: OracleCfg, seed: int, gid: int, episode: int):
     t3 = np.zeros(3, np.float32)
     lib().oracle_reset_draw(C.byref(cfg), seed, gid, episode, _fp(i12), _fp(t3))
     return i12, t3
+
+
+def reset_draw_batch(cfg: OracleCfg, seed: int, gids, episodes):
+    """reset_draw for many (global env id, episode) pairs: (init12 [n,12], target3 [n,3])."""
+    g = np.ascontiguousarray(gids, np.uint64)
+    e = np.ascontiguousarray(episodes, np.uint32)
+    n = len(g)
+    i12 = np.zeros((n, 12), np.float32)
+    t3 = np.zeros((n, 3), np.float32)
+    lib().oracle_reset_draw_batch(C.byref(cfg), seed, g.ctypes.data, e.ctypes.data, n, _fp(i12), _fp(t3))
+    return i12, t3
+
+
+def reset_obs_batch(cfg: OracleCfg, seed: int, gids, episodes):
+    """The reset observation of each (global env id, episode) draw: Env.reset_with(reset_draw(...))."""
+    i12, t3 = reset_draw_batch(cfg, seed, gids, episodes)
+    n = len(i12)
+    envs = (OracleEnv * n)()
+    obs = np.zeros((n, 12), np.float32)
+    lib().oracle_env_reset_batch(C.byref(cfg), envs, n, _fp(i12), _fp(t3), _fp(obs))
+    return obs
+
+
+def _as_struct_array(arr, ctype):
+    import warnings
+    with warnings.catch_warnings():  # ctypes' PEP 3118 format of a padded struct: numpy guesses right
+        warnings.simplefilter("ignore", RuntimeWarning)
+        v = np.ctypeslib.as_array(arr)
+    assert v.dtype.itemsize == C.sizeof(ctype)
+    return v
+
+
+def step_batch(cfg: OracleCfg, st: dict, acts) -> dict:
+    """One oracle step of many envs from the given float32 states (the dict of QuadVecEnv.get_state:
+    qpos [n,11], qvel [n,10], voltage [n], target [n,3], step_count [n], rate_int [n,3],
+    optionally prev_action [n,4]) -- Env.set_full_state + Env.step per row, in C. Returns the step
+    outputs (obs, reward, terminated, truncated, state12, motor_commands, voltage, voltage_scale,
+    env_action, obs7) and the post-step qpos / qvel / rate_int, as arrays over the rows."""
+    a = np.ascontiguousarray(acts, np.float32)
+    n = len(a)
+    envs = (OracleEnv * n)()
+    v = _as_struct_array(envs, OracleEnv)
+    v["qpos"] = np.asarray(st["qpos"], np.float32)
+    v["qvel"] = np.asarray(st["qvel"], np.float32)
+    v["voltage"] = np.asarray(st["voltage"], np.float32)
+    v["target"] = np.asarray(st["target"], np.float32)
+    v["step_count"] = np.asarray(st["step_count"], np.int32)
+    v["rate_int"] = np.asarray(st.get("rate_int", np.zeros((n, 3))), np.float32)
+    v["prev_action"] = np.asarray(st.get("prev_action", np.zeros((n, 4))), np.float32)
+    L = lib()
+    L.oracle_env_prepare_batch(C.byref(cfg), envs, n)
+    outs = (OracleStepOut * n)()
+    L.oracle_env_step_batch(C.byref(cfg), envs, n, _fp(a), outs)
+    o = _as_struct_array(outs, OracleStepOut)
+    res = {k: np.array(o[k]) for k in o.dtype.names}
+    res["terminated"] = res["terminated"].astype(bool)
+    res["truncated"] = res["truncated"].astype(bool)
+    res.update(qpos=np.array(v["qpos"]), qvel=np.array(v["qvel"]), rate_int=np.array(v["rate_int"]),
+               step_count=np.array(v["step_count"]))
+    return res
 
 
 def random_action(seed: int, gid: int, step: int):

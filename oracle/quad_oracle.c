@@ -766,6 +766,19 @@ void oracle_env_step_batch(const OracleCfg* cfg, OracleEnv* envs, int32_t n,
   for (int32_t i = 0; i < n; i++) oracle_env_step(cfg, envs + i, actions + 4 * i, outs + i);
 }
 
+/* Batch helpers for the large-N parity tests (test infrastructure only): derive every env's
+ * state12 from its (qpos, qvel) as set_full_state does, and reset a batch from given draws. */
+void oracle_env_prepare_batch(const OracleCfg* cfg, OracleEnv* envs, int32_t n) {
+  float obs[12];
+  for (int32_t i = 0; i < n; i++) oracle_get_obs(cfg, envs + i, obs);
+}
+
+void oracle_env_reset_batch(const OracleCfg* cfg, OracleEnv* envs, int32_t n, const float* init12,
+                            const float* target3, float* obs) {
+  for (int32_t i = 0; i < n; i++)
+    oracle_env_reset(cfg, envs + i, init12 + 12 * (size_t)i, target3 + 3 * (size_t)i, obs + 12 * (size_t)i);
+}
+
 /* ---------------------------------------------------------------------------------------
  * Philox4x32-10 and the device draw mapping (restated for reset/action parity)
  * ------------------------------------------------------------------------------------- */
@@ -804,6 +817,12 @@ void oracle_reset_draw(const OracleCfg* cfg, uint64_t seed, uint64_t gid, uint32
     const float m = u01(r[12 + i]) * w;
     target3[i] = cfg->target_low[i] + m;
   }
+}
+
+void oracle_reset_draw_batch(const OracleCfg* cfg, uint64_t seed, const uint64_t* gid,
+                             const uint32_t* episode, int32_t n, float* init12, float* target3) {
+  for (int32_t i = 0; i < n; i++)
+    oracle_reset_draw(cfg, seed, gid[i], episode[i], init12 + 12 * (size_t)i, target3 + 3 * (size_t)i);
 }
 
 void oracle_random_action(uint64_t seed, uint64_t gid, uint32_t step, float a[4]) {

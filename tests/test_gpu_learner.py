@@ -435,3 +435,43 @@ def test_split_kernels_match_combined(monkeypatch):
     for a, b in zip(out[0][0], out[1][0]):
         assert torch.equal(a, b)
     assert torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("norm", [True, False])
+def test_precomputed_adv_stats_are_bit_identical(norm, learner_form):
+    """The data-parallel overlap (ppo/ppo.py _train_fused): quad_ppo_adv_stats for minibatch k+1 is
+    enqueued while minibatch k's all-reduce is in flight, and grads(..., adv_ready=True) then skips
+    its own statistics pre-pass (QUAD_ADV_PRECOMPUTED). That must give the same bits as the normal
+    launch sequence -- every gradient tensor and the loss statistics -- for both learner forms; and
+    the precomputed path must really read what adv_stats wrote (stats of another minibatch give a
+    different gradient)."""
+    from uav_reinforcement_learning_control_amd.ppo.learner import FusedLearner, _ordered
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig
+    cfg = PPOConfig(normalize_advantage=norm)
+    pol = _policy(21)
+    M, B = 50000, 32768 + 77
+    obs, act, logp_old, adv, ret = _buffers(pol, M, 21, cfg.clip_range)
+    perm = torch.randperm(M, generator=torch.Generator().manual_seed(3)).cuda()
+    idx, other = perm[:B].contiguous(), perm[M - B:].contiguous()
+    fl = FusedLearner(pol, cfg.clip_range, cfg.ent_coef, cfg.vf_coef, norm)
+
+    def run(pre, ready):
+        for p in pol.parameters():
+            p.grad = torch.full_like(p, 7.0)
+        st = torch.zeros(4, device="cuda")
+        if pre is not None:
+            fl.adv_stats(adv, pre)
+        fl.grads(obs, act, logp_old, adv, ret, idx, st, adv_ready=ready)
+        torch.cuda.synchronize()
+        return [p.grad.clone() for p in _ordered(pol)], st.clone()
+
+    g0, s0 = run(None, False)
+    g1, s1 = run(idx, True)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
+    assert torch.equal(s0, s1)
+    g2, _ = run(other, True)  # another minibatch's mean / std
+    if norm:
+        assert any(not torch.equal(a, b) for a, b in zip(g0, g2))
+    else:  # without normalization there are no statistics to use: the flag changes nothing
+        assert all(torch.equal(a, b) for a, b in zip(g0, g2))

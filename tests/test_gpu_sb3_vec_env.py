@@ -1,0 +1,116 @@
+"""The SB3 VecEnv facade (envs/sb3_vec_env.py) against QuadVecEnv's own tensors, bit for bit.
+
+Reference caller: train.py:48-50 -- make_vec_env(make_env, n_envs) handed to SB3 PPO, whose
+collect_rollouts calls env.step(clipped_actions) -> (obs, rewards, dones, infos) and reads
+infos[i]["terminal_observation"] / ["TimeLimit.truncated"] / ["episode"] (SB3 DummyVecEnv +
+Monitor semantics, restated in the facade's docstring).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _make(max_steps=20, wrapper=True):
+    from uav_reinforcement_learning_control_amd.envs import HoverEnv, RateControlWrapper
+
+    def make_env():
+        env = HoverEnv(device="cuda:0", max_episode_steps=max_steps)
+        return RateControlWrapper(env) if wrapper else env
+    return make_env
+
+
+@pytest.mark.parametrize("wrapper", [True, False])
+def test_sb3_facade_matches_quadvecenv(wrapper):
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv, make_vec_env
+    n, T, seed = 4096, 45, 3
+    venv = make_vec_env(_make(wrapper=wrapper), n_envs=n, seed=seed)
+    ref = QuadVecEnv(n, wrapper="RateControlWrapper" if wrapper else None, device="cuda:0", seed=seed,
+                     max_episode_steps=20)
+    assert venv.num_envs == n and venv.observation_space.shape == (12,) and venv.action_space.shape == (4,)
+    assert venv.venv.cfg.wrapper == ref.cfg.wrapper and venv.venv.max_episode_steps == 20
+    o = venv.reset()
+    assert isinstance(o, np.ndarray) and o.shape == (n, 12)
+    assert np.array_equal(o.view(np.uint32), ref.reset().cpu().numpy().view(np.uint32))
+    ep_ret = np.zeros(n)
+    ep_len = np.zeros(n, np.int64)
+    finished = truncs = 0
+    for t in range(T):
+        acts = ref.random_actions(t)
+        a_np = acts.cpu().numpy()
+        if t % 2:
+            obs, rew, dones, infos = venv.step(a_np)
+        else:
+            venv.step_async(a_np)
+            obs, rew, dones, infos = venv.step_wait()
+        r_obs, r_rew, r_te, r_tr, r_inf = ref.step(acts)
+        r_done = (r_te | r_tr).cpu().numpy()
+        assert np.array_equal(obs.view(np.uint32), r_obs.cpu().numpy().view(np.uint32)), t
+        assert np.array_equal(rew.view(np.uint32), r_rew.cpu().numpy().view(np.uint32)), t
+        assert dones.dtype == np.bool_ and np.array_equal(dones, r_done), t
+        assert isinstance(infos, list) and len(infos) == n
+        tobs = r_inf["terminal_observation"].cpu().numpy()
+        tl = r_inf["TimeLimit.truncated"].cpu().numpy()
+        ep_ret += r_rew.cpu().numpy().astype(np.float64)
+        ep_len += 1
+        for i in range(n):
+            if r_done[i]:
+                inf = infos[i]
+                assert np.array_equal(inf["terminal_observation"], tobs[i]), (t, i)
+                assert inf["TimeLimit.truncated"] == bool(tl[i])
+                assert inf["episode"]["r"] == ep_ret[i] and inf["episode"]["l"] == ep_len[i]
+                truncs += int(tl[i])
+            else:
+                assert infos[i] == {}
+        finished += int(r_done.sum())
+        ep_ret[r_done] = 0.0
+        ep_len[r_done] = 0
+    assert finished > n and truncs > 0  # terminations and 20-step time limits both occurred
+    # attribute / method access with SB3's index semantics
+    assert venv.get_attr("max_episode_steps") == [20] * n
+    assert venv.get_attr("dt", indices=[0, 5]) == [ref.dt] * 2
+    rows = venv.env_method("random_actions", 7, indices=[3, 9])
+    full = ref.random_actions(7)
+    assert torch.equal(rows[0], full[3]) and torch.equal(rows[1], full[9])
+    from uav_reinforcement_learning_control_amd.envs import RateControlWrapper, RelPosActWrapper
+    assert venv.env_is_wrapped(RateControlWrapper, indices=[0]) == [wrapper]
+    assert venv.env_is_wrapped(RelPosActWrapper, indices=[0]) == [False]
+    # seed() takes effect at the next reset, as in SB3
+    assert venv.seed(11)[:2] == [11, 12]
+    assert np.array_equal(venv.reset(), ref.reset(seed=11).cpu().numpy())
+    venv.close(); ref.close()
+
+
+def test_sb3_facade_tensor_mode_and_relpos_stack():
+    """as_tensors=True keeps the outputs on the GPU; the README stack RelPosActWrapper(
+    RateControlWrapper(HoverEnv())) becomes the combined kernel kind with 7-D obs."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    from uav_reinforcement_learning_control_amd.envs import (HoverEnv, QuadVecEnv, RateControlWrapper,
+                                                             RelPosActWrapper, make_vec_env)
+    n = 1000
+    venv = make_vec_env(lambda: RelPosActWrapper(RateControlWrapper(HoverEnv(device="cuda:0"))), n_envs=n,
+                        seed=4, as_tensors=True)
+    assert venv.venv.cfg.wrapper == N.WRAP_CTBR_RELPOS and venv.observation_space.shape == (7,)
+    ref = QuadVecEnv(n, wrapper="ctbr_relpos", device="cuda:0", seed=4)
+    o = venv.reset()
+    assert torch.is_tensor(o) and o.is_cuda and torch.equal(o, ref.reset())
+    for t in range(5):
+        a = ref.random_actions(t)
+        obs, rew, dones, infos = venv.step(a)
+        r_obs, r_rew, te, tr, _ = ref.step(a)
+        assert torch.equal(obs, r_obs) and torch.equal(rew, r_rew) and torch.equal(dones, te | tr)
+    venv.close(); ref.close()
+
+
+def test_sb3_facade_rejects_non_autoreset():
+    from uav_reinforcement_learning_control_amd.envs import QuadSB3VecEnv, QuadVecEnv
+    env = QuadVecEnv(64, device="cuda:0", auto_reset=False)
+    with pytest.raises(ValueError):
+        QuadSB3VecEnv(env)
+    venv = QuadSB3VecEnv(QuadVecEnv(64, device="cuda:0"))
+    with pytest.raises(RuntimeError):
+        venv.step_wait()
+    with pytest.raises(ValueError):
+        venv.set_attr("max_episode_steps", 3, indices=[0])
+    venv.close(); env.close()

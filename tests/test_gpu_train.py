@@ -128,6 +128,20 @@ def test_relpos_over_rate_control_stack():
     w.close(); d.close()
     with pytest.raises(TypeError):
         RateControlWrapper(RelPosActWrapper(HoverEnv(device="cuda:0")))
+    # the intermediate RateControlWrapper now passes obs7 up: its space says so
+    w = RelPosActWrapper(RateControlWrapper(QuadVecEnv(64, device="cuda:0", seed=4)))
+    assert w.env.observation_space.shape == (7,) and w.observation_space.shape == (7,)
+    w.close()
+    # envs BUILT with the CTBR kind keep the rate controller under RelPosActWrapper (no silent
+    # downgrade to raw torques); an observation wrapper twice is refused
+    for base in (QuadVecEnv(64, wrapper="ctbr", device="cuda:0", seed=4),
+                 HoverEnv(device="cuda:0", wrapper="RateControlWrapper")):
+        w = RelPosActWrapper(base)
+        vec = w.env if isinstance(w.env, QuadVecEnv) else w.unwrapped._vec
+        assert vec.cfg.wrapper == N.WRAP_CTBR_RELPOS
+        with pytest.raises(TypeError):
+            RelPosActWrapper(w.env)
+        w.close()
 
 
 @pytest.mark.parametrize("one_launch", [True, False])
@@ -156,5 +170,12 @@ def test_resume_draws_fresh_noise(one_launch):
 
     sd, (a_first, a_second) = run(rollouts=2)
     assert sd["noise_step"] == 2 * 16
-    _, (b_first,) = run(sd)  # same params, same env seed: only the noise can differ
+    sd_b, (b_first,) = run(sd)  # same params, same env seed: only the noise can differ
     assert not torch.equal(b_first, a_first)  # not a replay of the original run's first rollout
+    # where the counter resumed: the rollout after the checkpoint consumed noise steps 32 .. 47
+    assert sd_b["noise_step"] == 2 * 16 + 16
+    # a checkpoint between rollout boundaries: the one-launch path continues at the saved step, the
+    # two-launch path (whose cursor also selects the buffer row t % n_steps) at the next boundary
+    sd_mid = dict(sd, noise_step=20)
+    sd_c, _ = run(sd_mid)
+    assert sd_c["noise_step"] == (20 + 16 if one_launch else 32 + 16)

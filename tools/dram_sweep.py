@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""A/B of the large-batch step forms (QUADENV_LANES = 1 / 2 / 4 lanes per env, SPEC constants on
+when the handle is a reference default) from 262,144 to 8,388,608 envs: graph-replayed launches
+after the post-reset transient, HIP-event timing (bench.py's gated method). Prints one JSON line per
+point; feeds quad_create's per-size choice of the lanes per env."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+
+def point(n, lanes, launches):
+    os.environ["QUADENV_LANES"] = str(lanes)
+    from bench import _gated_kernel_us, _kernel_symbol, _quad_step_fn
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    e = QuadVecEnv(n, env="hover", device="cuda:0", seed=0)
+    e.reset()
+    acts = [e.random_actions(k) for k in range(8)]
+    st = _quad_step_fn(e)
+    for k in range(50):
+        st(acts[k % 8].data_ptr())
+    us = _gated_kernel_us(st, acts, launches)
+    sym = _kernel_symbol(e)
+    e.close()
+    del acts
+    torch.cuda.empty_cache()
+    return us, sym
+
+
+if __name__ == "__main__":
+    sizes = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else \
+        [1 << 18, 1 << 19, 1 << 20, 1 << 21, 1 << 22, 1 << 23]
+    lanes_list = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 4]
+    for n in sizes:
+        for lanes in lanes_list:
+            launches = 200 if n <= (1 << 20) else 100 if n <= (1 << 22) else 100
+            us, sym = point(n, lanes, launches)
+            gbs = 278 * n / (us * 1e-6) / 1e9
+            print(json.dumps({"envs": n, "lanes": lanes, "kernel": sym, "kernel_us": round(us, 2),
+                              "GBs": round(gbs, 1), "frac": round(gbs / 8000, 3)}), flush=True)

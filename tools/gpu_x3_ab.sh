@@ -15,7 +15,7 @@ step() {  # name timeout cmd...
   return 0
 }
 step x3_bits 300 python -u tools/x3_bits_ab.py tools/_build/x3_old.so tools/_build/x3_new.so
-step x3_time 500 bash tools/x3_share_sweep.sh ${X3_SHARES:-}
+step x3_time 500 bash tools/x3_ab_time.sh
 [ -n "${X3_TESTS:-1}" ] && step learner_tests 600 python -u -m pytest tests/test_gpu_learner.py -q -rf --timeout 300 --timeout-method thread
 [ -f tools/_build/lprobe.so ] && step lprobe 300 python -u tools/probe/probe_learner.py
 echo "=== done"

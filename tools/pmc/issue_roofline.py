@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Summarize tools/pmc/issue_roofline.sh into profiles/<round>/pmc_issue.json and
-profiles/pmc_issue.json (bench.py reads the latter into roofline.issue).
+profiles/pmc_issue.json (bench.py reads the latter into roofline.issue), keyed by the kernel's
+template symbol and the env count: {"round": ..., "kernels": {symbol: {envs: record}}}, so the
+bench attaches a record only to the kernel it timed.
 
 Per step-kernel dispatch (median over dispatches 20..end, past the post-reset transient):
   instructions per 64 env-steps by class (SQ_INSTS_* / (envs / 64)): one step wave of 64 envs,
@@ -44,14 +46,10 @@ def trace_us(root):
     return out
 
 
-def main(root="gpurun_out/issue", rnd="r02"):
+def main(root="gpurun_out/issue", rnd="r04"):
     res = {}
-    traces = {}
-    for name, n in (("trace", 65536), ("trace1m", 1048576)):
-        t = trace_us(os.path.join(root, name))
-        if t:
-            traces[n] = list(t.values())[0]
-    for n in (65536, 1048576):
+    sizes = sorted(int(m.group(1)) for m in (re.match(r"n(\d+)$", x) for x in os.listdir(root)) if m)
+    for n in sizes:
         d = load(os.path.join(root, f"n{n}"))
         if not d:
             continue
@@ -62,8 +60,9 @@ def main(root="gpurun_out/issue", rnd="r02"):
         per_wave = {k[len("SQ_INSTS_"):].lower(): c[k] / units for k in c if k.startswith("SQ_INSTS_")}
         vec = per_wave.get("valu", 0) + per_wave.get("vmem_rd", 0) + per_wave.get("vmem_wr", 0) + per_wave.get("lds", 0)
         sca = per_wave.get("salu", 0) + per_wave.get("smem", 0) + per_wave.get("branch", 0)
-        us = traces.get(n)
-        r = {"kernel": key[0], "grid": key[1], "envs": n, "waves": waves, "waves_per_64_envs": waves / units,
+        t = trace_us(os.path.join(root, f"trace_{n}"))
+        us = list(t.values())[0] if t else None
+        r = {"grid": key[1], "envs": n, "waves": waves, "waves_per_64_envs": waves / units,
              "instructions_per_64_env_steps": per_wave, "vector_instructions_per_64_env_steps": vec,
              "scalar_instructions_per_64_env_steps": sca, "kernel_us_rocprof_trace": us}
         if "SQ_WAVE_CYCLES" in c:
@@ -82,11 +81,13 @@ def main(root="gpurun_out/issue", rnd="r02"):
             clk = c["GRBM_GUI_ACTIVE"] / 8 / (us * 1e3)
             if clk <= 2.5:
                 r["effective_clock_GHz"] = clk
-        res[str(n)] = r
+        res.setdefault(key[0], {})[str(n)] = r
+    out = {"round": rnd, "source": "tools/pmc/issue_roofline.sh (rocprofv3 PMC over tools/step_once.py)",
+           "kernels": res}
     for d in (os.path.join("profiles", rnd), "profiles"):
         os.makedirs(d, exist_ok=True)
-        json.dump(res, open(os.path.join(d, "pmc_issue.json"), "w"), indent=1)
-    print(json.dumps(res, indent=1))
+        json.dump(out, open(os.path.join(d, "pmc_issue.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":

@@ -1582,6 +1582,7 @@ struct QuadHandle {
   KConsts<float>* kdev = nullptr;    // device copy the kernels read (scalar loads, K$-resident)
   bool spec = false;                 // kh == a reference default block: k_step's SPEC form
   bool helper = true;                // one-thread form: k_step_h (helper waves draw the resets)
+  int hblock = 0;                    // envs per k_step_h block: 0 = by size (64 up to H_SMALL, else 256)
 };
 
 namespace {
@@ -1652,6 +1653,11 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   // measured: helper waves 6.54 -> 5.87 us at 65,536 envs, 5.74 -> 4.24 at 4,096;
   // QUADENV_HELPER=0 keeps the plain k_step (A/B and tests)
   if (const char* v = std::getenv("QUADENV_HELPER")) h->helper = std::atoi(v) != 0;
+  // QUADENV_HBLOCK=64|256 pins the helper form's block size (tests run the 256-env blocks at small N)
+  if (const char* v = std::getenv("QUADENV_HBLOCK")) {
+    const int b = std::atoi(v);
+    if (b == 64 || b == 256) h->hblock = b;
+  }
   h->device = device;
   h->n = n_envs;
   DeviceGuard g(device);
@@ -1701,7 +1707,9 @@ int32_t quad_kernel_form(const QuadHandle* h) {
   // RELPOS and the brax kinds have one kernel each (k_step_relpos / k_step_brax): no lanes, SPEC
   // or helper forms to report
   if (wrap_relpos(h->cfg.wrapper) || h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) return 64;
-  return h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0);
+  const bool wide = h->hblock ? h->hblock == 256 : h->n > H_SMALL;
+  return h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0) |
+         (h->lanes == 0 && h->helper && wide ? 128 : 0);
 }
 
 int quad_seed(QuadHandle* h, uint64_t seed, void* stream) {
@@ -1797,7 +1805,8 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, true, SP, HB>), grid, blk2, 0, s, QD_KARGS);     \
   else                                                                                          \
     hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, false, SP, HB>), grid, blk2, 0, s, QD_KARGS);
-    if (h->helper && count <= H_SMALL) {
+    const bool wide = h->hblock ? h->hblock == 256 : count > H_SMALL;
+    if (h->helper && !wide) {
       const dim3 grid(unsigned((int64_t(count) + 63) / 64)), blk2(128);
       if (h->spec) { QD_LAUNCH_H(true, 64) } else { QD_LAUNCH_H(false, 64) }
     } else if (h->helper) {
@@ -1821,7 +1830,9 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG, SP>), grid, blk, 0, s, QD_GARGS);
     if (G == 1) {  // the batch-size default above 262,144 envs: SPEC form when the block is the default
       if (h->spec) { QD_LAUNCH(1, true) } else { QD_LAUNCH(1, false) }
-    } else if (G == 2) { QD_LAUNCH(2, false) } else { QD_LAUNCH(4, false) }
+    } else if (G == 2) {
+      if (h->spec) { QD_LAUNCH(2, true) } else { QD_LAUNCH(2, false) }
+    } else { QD_LAUNCH(4, false) }
 #undef QD_LAUNCH
 #undef QD_GARGS
   }
@@ -1910,7 +1921,8 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
     hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, true, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
   else                                                                                                   \
     hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, false, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-  if (h->helper && h->n <= H_SMALL) {
+  const bool wide = h->hblock ? h->hblock == 256 : h->n > H_SMALL;
+  if (h->helper && !wide) {
     const dim3 grid(unsigned((int64_t(h->n) + 63) / 64)), blk2(128);
     if (h->spec) { QD_LAUNCH_RH(true, 64) } else { QD_LAUNCH_RH(false, 64) }
   } else if (h->helper) {

@@ -44,7 +44,11 @@ def _gain_overrides(max_rate, kd, ki_rate_torque, integral_max):
 
 
 def _wrapper_of(env):
-    return env.wrapper if isinstance(env, QuadVecEnv) else env._vec.wrapper
+    if isinstance(env, QuadVecEnv):
+        return env.wrapper
+    if isinstance(env, HoverEnv):
+        return env._vec.wrapper
+    raise TypeError(f"cannot wrap {type(env).__name__}")
 
 
 class RateControlWrapper:

@@ -22,14 +22,24 @@ class RelPosActWrapper:
 
     def __init__(self, env):
         from ..utils.spaces import Box
-        from .rate_wrapper import rebuild
+        from .rate_wrapper import _wrapper_of, rebuild
         if isinstance(env, RateControlWrapper):
             old = env.env
             env.env = rebuild(old, "ctbr_relpos")  # gains travel in the cfg overrides
             old.close()
+            env.observation_space = env.env.observation_space  # the wrapper below now returns obs7
             self.env = env
         else:
-            inner = rebuild(env, "RelPosActWrapper")
+            # an env built with a wrapper kind already: CTBR stacks (the rate controller must stay in
+            # the step), an observation wrapper twice is refused
+            kind = _wrapper_of(env)
+            if kind in ("RateControlWrapper", "ctbr"):
+                target = "ctbr_relpos"
+            elif kind in (None, "none"):
+                target = "RelPosActWrapper"
+            else:
+                raise TypeError(f"RelPosActWrapper: the env already has the {kind!r} wrapper kind")
+            inner = rebuild(env, target)
             env.close()
             self.env = inner
         self.observation_space = Box(-1.0, 1.0, (7,), np.float32)
