@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define QUADENV_ABI_VERSION 4
+#define QUADENV_ABI_VERSION 5
 
 enum { QUAD_OK = 0, QUAD_EINVAL = -1, QUAD_EHIP = -2, QUAD_ENOMEM = -3, QUAD_EMODEL = -4 };
 /* QUAD_ENV_BRAX_HOVER / QUAD_ENV_BRAX_TRAJ: the brax Env API siblings of the same path
@@ -376,9 +376,12 @@ typedef struct QuadPPOBatch {
   const int64_t* index;     /* [batch] rows of this minibatch, each in [0, M) */
   int32_t batch;            /* >= 1 */
   int32_t normalize_advantage;  /* 0: off; 1: on; QUAD_ADV_PRECOMPUTED: on, and quad_ppo_adv_stats already
-                                   wrote this minibatch's sums into the same workspace (stream-ordered) */
+                                   wrote this minibatch's sums into the same workspace (stream-ordered);
+                                   QUAD_ADV_GIVEN: on, with the sums in adv_sums */
   float clip_range, ent_coef, vf_coef;
   float* stats;             /* [4] out, or NULL: pg_loss, vf_loss, entropy, clip_fraction */
+  const double* adv_sums;   /* QUAD_ADV_GIVEN: this minibatch's [QUAD_ADV_SUM_DOUBLES] block sums (a slice of
+                               quad_ppo_adv_stats_epoch's output); ignored otherwise (ABI v5) */
 } QuadPPOBatch;
 
 /* ---- The optimizer step of PPO.train (row P), fused: torch.nn.utils.clip_grad_norm_(params,
@@ -422,8 +425,17 @@ int quad_ppo_grad(const QuadPolicyParams* params, const QuadPPOBatch* b, const Q
  * float64), on their own: a data-parallel learner enqueues them for the NEXT minibatch while the
  * gradient all-reduce of this one is in flight (they read only advantages[index]), then calls
  * quad_ppo_grad with normalize_advantage = QUAD_ADV_PRECOMPUTED and the same workspace. */
-enum { QUAD_ADV_PRECOMPUTED = 2 };
+enum { QUAD_ADV_PRECOMPUTED = 2, QUAD_ADV_GIVEN = 3 };
 int quad_ppo_adv_stats(const QuadPPOBatch* b, void* workspace, int64_t workspace_bytes, void* stream);
+/* The same statistics for every minibatch of an epoch in ONE launch (SB3 PPO.train normalizes each
+ * minibatch by its own mean / std; minibatch m is rows perm[m * batch .. (m + 1) * batch) of the
+ * epoch permutation): sums[m * QUAD_ADV_SUM_DOUBLES ...] receives minibatch m's block sums in the
+ * fixed order quad_ppo_adv_stats uses, so quad_ppo_grad with normalize_advantage = QUAD_ADV_GIVEN and
+ * adv_sums = that slice gives bit-identical gradients. One full-occupancy launch per epoch instead
+ * of n_minibatches latency-bound 256-block pre-passes. */
+#define QUAD_ADV_SUM_DOUBLES 512
+int quad_ppo_adv_stats_epoch(const float* advantages, const int64_t* perm, int32_t batch, int32_t n_minibatches,
+                             double* sums, void* stream);
 /* Diagnostics (parity tests): quad_ppo_grad through a build of the same kernel body that also
  * records the hidden pre-activations (before the ReLU) it computed for every minibatch row:
  * hidden[(net * batch + pos) * 256 + 128 * layer + neuron], net 0 = actor / 1 = critic, pos = the

@@ -16,9 +16,11 @@ CSRC = os.path.join(_PKG, "csrc")
 
 QUAD_OK, QUAD_EINVAL, QUAD_EHIP, QUAD_ENOMEM, QUAD_EMODEL = 0, -1, -2, -3, -4
 QUAD_ADV_PRECOMPUTED = 2  # QuadPPOBatch.normalize_advantage: quad_ppo_adv_stats already ran
+QUAD_ADV_GIVEN = 3        # ... : the sums are in QuadPPOBatch.adv_sums (quad_ppo_adv_stats_epoch)
+ADV_SUM_DOUBLES = 512     # QUAD_ADV_SUM_DOUBLES: one minibatch's block sums
 ENV_HOVER, ENV_TRAJ, ENV_BRAX_HOVER, ENV_BRAX_TRAJ = 0, 1, 2, 3
 WRAP_NONE, WRAP_CTBR, WRAP_RELPOS, WRAP_CTBR_RELPOS = 0, 1, 2, 3
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class QuadCfg(C.Structure):
@@ -99,7 +101,7 @@ EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_crea
            "quad_kernel_form", "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
            "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
            "quad_waypoints_begin", "quad_waypoints_update", "quad_ppo_workspace_bytes", "quad_ppo_grad",
-           "quad_ppo_grad_form", "quad_ppo_hidden", "quad_ppo_adv_stats", "quad_permutation", "quad_adam_workspace_bytes",
+           "quad_ppo_grad_form", "quad_ppo_hidden", "quad_ppo_adv_stats", "quad_ppo_adv_stats_epoch", "quad_permutation", "quad_adam_workspace_bytes",
            "quad_clip_adam")
 
 
@@ -120,7 +122,7 @@ class QuadPolicyGrads(C.Structure):
 class QuadPPOBatch(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("obs", "actions", "log_prob", "advantages", "returns", "index")] + \
                [("batch", C.c_int32), ("normalize_advantage", C.c_int32), ("clip_range", C.c_float),
-                ("ent_coef", C.c_float), ("vf_coef", C.c_float), ("stats", C.c_void_p)]
+                ("ent_coef", C.c_float), ("vf_coef", C.c_float), ("stats", C.c_void_p), ("adv_sums", C.c_void_p)]
 
 
 ADAM_MAX_TENSORS = 16
@@ -181,10 +183,11 @@ def _declare(L):
     L.quad_ppo_hidden.argtypes = [C.POINTER(QuadPolicyParams), C.POINTER(QuadPPOBatch), C.POINTER(QuadPolicyGrads),
                                   vp, vp, C.c_int64, vp]
     L.quad_ppo_adv_stats.argtypes = [C.POINTER(QuadPPOBatch), vp, C.c_int64, vp]
+    L.quad_ppo_adv_stats_epoch.argtypes = [vp, vp, C.c_int32, C.c_int32, vp, vp]
     L.quad_adam_workspace_bytes.argtypes = [C.POINTER(QuadAdam)]
     L.quad_adam_workspace_bytes.restype = C.c_int64
     L.quad_clip_adam.argtypes = [C.POINTER(QuadAdam), vp, C.c_int64, vp]
-    for n in ("quad_clip_adam", "quad_ppo_grad", "quad_ppo_hidden", "quad_ppo_adv_stats", "quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe", "quad_terminated", "quad_step_random",
+    for n in ("quad_clip_adam", "quad_ppo_grad", "quad_ppo_hidden", "quad_ppo_adv_stats", "quad_ppo_adv_stats_epoch", "quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe", "quad_terminated", "quad_step_random",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
               "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
               "quad_waypoints_begin", "quad_waypoints_update"):

@@ -443,6 +443,15 @@ __global__ __launch_bounds__(256) void k_adv_stats(const float* __restrict__ adv
   adv_stats_block(adv, idx, batch, part, blockIdx.x, red);
 }
 
+// every minibatch of an epoch: block (b, m) is block b of minibatch m's statistics
+__global__ __launch_bounds__(256) void k_adv_stats_epoch(const float* __restrict__ adv, const int64_t* __restrict__ perm,
+                                                         int batch, double* __restrict__ sums) {
+  __shared__ double red[2][256];
+  const size_t m = blockIdx.y;
+  adv_stats_block(adv, perm + m * size_t(batch), batch, sums + m * QUAD_ADV_SUM_DOUBLES, blockIdx.x, red);
+}
+static_assert(QUAD_ADV_SUM_DOUBLES == 2 * ADV_BLOCKS, "ABI constant");
+
 struct RArgs {
   QuadPolicyGrads gr;
   const float* part;
@@ -691,7 +700,11 @@ int ppo_grad_impl(const QuadPolicyParams* p, const QuadPPOBatch* b, const QuadPo
   double* adv_part = static_cast<double*>(workspace);
   float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) + l.adv_bytes);
   const bool norm = b->normalize_advantage && b->batch > 1;
-  const bool need_stats = norm && b->normalize_advantage != QUAD_ADV_PRECOMPUTED;  // (2: quad_ppo_adv_stats ran)
+  const bool given = b->normalize_advantage == QUAD_ADV_GIVEN;  // (3: quad_ppo_adv_stats_epoch's slice)
+  if (norm && given && !b->adv_sums) return lfail(QUAD_EINVAL, "QUAD_ADV_GIVEN needs adv_sums");
+  // (2: quad_ppo_adv_stats ran into the workspace; 3: the sums are given)
+  const bool need_stats = norm && b->normalize_advantage != QUAD_ADV_PRECOMPUTED && !given;
+  if (norm && given) adv_part = const_cast<double*>(b->adv_sums);
   if (need_stats && !x3) {  // the bf16x3 form computes them in its prep launch
     hipLaunchKernelGGL(k_adv_stats, dim3(ADV_BLOCKS), dim3(256), 0, s, b->advantages, b->index, b->batch, adv_part);
     if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_adv_stats launch failed");
@@ -744,6 +757,16 @@ int quad_ppo_adv_stats(const QuadPPOBatch* b, void* workspace, int64_t workspace
     hipLaunchKernelGGL(k_adv_stats, dim3(ADV_BLOCKS), dim3(256), 0, static_cast<hipStream_t>(stream), b->advantages,
                        b->index, b->batch, static_cast<double*>(workspace));
   if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_adv_stats launch failed");
+  return QUAD_OK;
+}
+
+int quad_ppo_adv_stats_epoch(const float* advantages, const int64_t* perm, int32_t batch, int32_t n_minibatches,
+                             double* sums, void* stream) {
+  if (!advantages || !perm || !sums) return lfail(QUAD_EINVAL, "NULL argument");
+  if (batch < 1 || n_minibatches < 1 || n_minibatches > 65535) return lfail(QUAD_EINVAL, "need batch >= 1, 1 <= n_minibatches <= 65535");
+  hipLaunchKernelGGL(k_adv_stats_epoch, dim3(ADV_BLOCKS, n_minibatches), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     advantages, perm, batch, sums);
+  if (hipGetLastError() != hipSuccess) return lfail(QUAD_EHIP, "k_adv_stats_epoch launch failed");
   return QUAD_OK;
 }
 

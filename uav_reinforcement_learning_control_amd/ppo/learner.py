@@ -74,16 +74,36 @@ class FusedLearner:
         N.check(self._lib.quad_ppo_adv_stats(C.byref(b), C.c_void_p(self._ws.data_ptr()), C.c_int64(self._ws.numel()),
                                              stream), "quad_ppo_adv_stats")
 
+    def adv_stats_epoch(self, advantages: torch.Tensor, perm: torch.Tensor, batch: int, n_minibatches: int,
+                        out: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        """The advantage statistics of every minibatch of an epoch in one launch
+        (quad_ppo_adv_stats_epoch): minibatch m = perm[m * batch:(m + 1) * batch]; row m of the
+        returned float64 [n_minibatches, 512] tensor is what grads(..., adv_sums=row) normalizes with
+        (bit-identical to the per-minibatch pre-pass). None without advantage normalization."""
+        if not self.normalize_advantage:
+            return None
+        if perm.dtype != torch.int64 or not perm.is_contiguous() or perm.numel() < batch * n_minibatches:
+            raise ValueError("perm: a contiguous int64 vector of at least batch * n_minibatches rows")
+        if out is None or tuple(out.shape) != (n_minibatches, N.ADV_SUM_DOUBLES):
+            out = torch.empty(n_minibatches, N.ADV_SUM_DOUBLES, dtype=torch.float64, device=self.device)
+        stream = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        N.check(self._lib.quad_ppo_adv_stats_epoch(C.c_void_p(advantages.data_ptr()), C.c_void_p(perm.data_ptr()),
+                                                   int(batch), int(n_minibatches), C.c_void_p(out.data_ptr()), stream),
+                "quad_ppo_adv_stats_epoch")
+        return out
+
     def grads(self, obs: torch.Tensor, actions: torch.Tensor, log_prob: torch.Tensor, advantages: torch.Tensor,
               returns: torch.Tensor, index: torch.Tensor, stats: Optional[torch.Tensor] = None,
-              hidden: Optional[torch.Tensor] = None, adv_ready: bool = False) -> None:
+              hidden: Optional[torch.Tensor] = None, adv_ready: bool = False,
+              adv_sums: Optional[torch.Tensor] = None) -> None:
         """Overwrite every parameter's .grad with the gradient of the PPO loss on rows `index` of the
         flattened buffers (obs [M,12], actions [M,4], log_prob / advantages / returns [M]).
         `stats` (float32 [4], optional) receives pg_loss, vf_loss, entropy, clip_fraction.
         `hidden` (float32 [2, B, 256], diagnostics): run the kernel's dump build (quad_ppo_hidden),
         which also records each row's hidden pre-activations [net][pos][h1 | h2].
-        `adv_ready`: adv_stats(advantages, index) was already enqueued for this minibatch (the
-        data-parallel overlap), so the launch sequence skips its own statistics pre-pass."""
+        `adv_ready`: adv_stats(advantages, index) was already enqueued for this minibatch, so the
+        launch sequence skips its own statistics pre-pass. `adv_sums`: this minibatch's row of
+        adv_stats_epoch (the statistics pre-pass is skipped; same bits)."""
         dev = self.device
         M = obs.shape[0]
         _need(obs, (M, 12), torch.float32, dev, "obs")
@@ -100,12 +120,17 @@ class FusedLearner:
         self._workspace(B)
         prm, grd = self._structs()
         norm = int(self.normalize_advantage)
-        if norm and adv_ready:
+        if norm and adv_sums is not None:
+            if adv_sums.dtype != torch.float64 or adv_sums.numel() != N.ADV_SUM_DOUBLES or not adv_sums.is_contiguous():
+                raise ValueError("adv_sums: one contiguous float64 row of adv_stats_epoch")
+            norm = N.QUAD_ADV_GIVEN
+        elif norm and adv_ready:
             norm = N.QUAD_ADV_PRECOMPUTED
         b = N.QuadPPOBatch(obs.data_ptr(), actions.data_ptr(), log_prob.data_ptr(), advantages.data_ptr(),
                            returns.data_ptr(), index.data_ptr(), B, norm,
                            self.clip_range, self.ent_coef, self.vf_coef,
-                           None if stats is None else stats.data_ptr())
+                           None if stats is None else stats.data_ptr(),
+                           adv_sums.data_ptr() if norm == N.QUAD_ADV_GIVEN else None)
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         if hidden is not None:
             _need(hidden, (2, B, 256), torch.float32, dev, "hidden")

@@ -398,26 +398,26 @@ class PPO:
         total = obs.shape[0]
         steps = epochs * nmb if max_minibatches is None else min(epochs * nmb, max_minibatches)
         mstats = torch.zeros(max(steps, 1), 4, dtype=torch.float32, device=self.device)
-        perms = {}
+        perms, sums = {}, {}
 
         def index_of(k):  # the k-th minibatch of the update: epoch k // nmb, slot k % nmb
             e, m = divmod(k, nmb)
             if e not in perms:  # drawn in epoch order, as the per-epoch loop drew them
                 perms[e] = epoch_permutation(total, self.device)
-            return perms[e][m * B:(m + 1) * B]
+                # every minibatch's advantage statistics of the epoch in one launch (the rollout
+                # buffer's advantages do not change during the update)
+                sums[e] = self._learner.adv_stats_epoch(adv, perms[e], B, nmb)
+            return perms[e][m * B:(m + 1) * B], (None if sums[e] is None else sums[e][m])
 
-        # data-parallel: the next minibatch's advantage statistics (they read only adv[index])
-        # run while this minibatch's gradient all-reduce is in flight
-        overlap = self.world > 1 and cfg.normalize_advantage
         done = 0
         for k in range(steps):
-            idx = index_of(k)
-            self._learner.grads(obs, act, logp_old, adv, ret, idx, mstats[k], adv_ready=overlap and k > 0)
+            idx, adv_sums = index_of(k)
+            self._learner.grads(obs, act, logp_old, adv, ret, idx, mstats[k], adv_sums=adv_sums)
             if self.world > 1:
-                nxt = (lambda: self._learner.adv_stats(adv, index_of(k + 1))) if overlap and k + 1 < steps else None
-                allreduce_mean_(self.params, self._flat, self.world, between=nxt)
+                allreduce_mean_(self.params, self._flat, self.world)
             self._adam.step()  # clip_grad_norm_ + Adam.step (quad_clip_adam)
             perms.pop(k // nmb - 1, None)
+            sums.pop(k // nmb - 1, None)
             done += 1
         a = mstats[:done].double().mean(0).tolist() if done else [0.0] * 4
         stats.update(pg_loss=a[0], vf_loss=a[1], entropy=a[2], clip_fraction=a[3], n=done)
