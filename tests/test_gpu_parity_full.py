@@ -29,7 +29,8 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from test_gpu_parity import _random_states, operand_only, parity_ok
+from test_gpu_parity import (OBS_SPAN, _random_states, euler_combination_ok, euler_slack, operand_only,
+                             parity_ok)
 
 pytestmark = pytest.mark.gpu
 
@@ -98,7 +99,11 @@ def _check_rows(g, ref, st, rows, what):
         elif k == "state12":
             pre = np.concatenate([st["qpos"][rows][:, :3], np.zeros((len(rows), 3), np.float32),
                                   st["qvel"][rows][:, :6]], 1)
-            note(k, parity_ok(g["state12"][rows], ref["state12"][rows], pre))
+            note(k, parity_ok(g["state12"][rows], ref["state12"][rows], pre, extra=euler_slack(ref["state12"][rows])))
+            note("roll-yaw", euler_combination_ok(g["state12"][rows], ref["state12"][rows]))
+        elif k == "obs":
+            # (reset rows carry the reset obs in both and are compared bit-exactly elsewhere)
+            note(k, parity_ok(g["obs"][rows], ref["obs"][rows], extra=euler_slack(ref["state12"][rows], OBS_SPAN)))
         else:
             gk, rk = g[k][rows], ref[k][rows]
             if gk.ndim == 1:

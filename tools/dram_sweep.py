@@ -13,6 +13,9 @@ import torch  # noqa: E402
 
 def point(n, lanes, launches):
     os.environ["QUADENV_LANES"] = str(lanes)
+    from uav_reinforcement_learning_control_amd import _native as N
+    if os.environ.get("QUADENV_LIB"):  # an A/B build (tools/probe/build_variant.sh)
+        N.LIB_PATH = os.environ["QUADENV_LIB"]
     from bench import _gated_kernel_us, _kernel_symbol, _quad_step_fn
     from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
     e = QuadVecEnv(n, env="hover", device="cuda:0", seed=0)
@@ -38,5 +41,5 @@ if __name__ == "__main__":
             launches = 200 if n <= (1 << 20) else 100 if n <= (1 << 22) else 100
             us, sym = point(n, lanes, launches)
             gbs = 278 * n / (us * 1e-6) / 1e9
-            print(json.dumps({"envs": n, "lanes": lanes, "kernel": sym, "kernel_us": round(us, 2),
+            print(json.dumps({"lib": os.environ.get("QUADENV_LIB", "in-tree"), "envs": n, "lanes": lanes, "kernel": sym, "kernel_us": round(us, 2),
                               "GBs": round(gbs, 1), "frac": round(gbs / 8000, 3)}), flush=True)

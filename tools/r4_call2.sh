@@ -14,6 +14,6 @@ step() {  # name timeout cmd...
 step r4_full 300 python -u -m pytest tests/test_gpu_parity_full.py -v -s --timeout 120 --timeout-method thread -p no:cacheprovider -k "step_matches or rollout_first or traj_ctbr"
 step r4_x3_bits 300 python -u tools/x3_bits_ab.py tools/_build/x3_old.so tools/_build/x3_new.so
 step r4_x3_time 500 bash tools/x3_ab_time.sh
-step r4_learner_tests 400 python -u -m pytest tests/test_gpu_learner.py -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider
+step r4_learner_tests 400 python -u -m pytest tests/test_gpu_learner.py tests/test_gpu_sb3_vec_env.py tests/test_gpu_train.py -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider
 step r4_dram_sweep 400 python -u tools/dram_sweep.py
 echo "=== done"

@@ -598,72 +598,12 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
     X3_BAR();  // B4: DH2 image complete
-    const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);  // dh1's first two k-steps
+    const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);  // dh1's first two k-steps: in flight through dW2
     LP(6);
 
-    // ---- dh1 (R form) = dh2 W2[:, block w] (relu'(h1) applied below); then the dW2 slab, whose
-    // 96 MFMAs carry the round's dW1 work in their issue gaps: the dh1 drain, relu'(h1), the splits
-    // of dh1 into dW1's A operand and dW1's 24 MFMAs (ordered after dW2 they were a serial VALU
-    // phase of ~1.9 k cycles per round at one wave per SIMD)
-    f32x16 dh1[2];
-#pragma unroll
-    for (int r = 0; r < 16; r++) { dh1[0][r] = 0.f; dh1[1][r] = 0.f; }
-    f32x16 dh1s[2] = {dh1[0], dh1[1]};
-#if !defined(QD_X3_NODH1)
-    {  // software pipeline as L2: A = DH2 row reads, B = pre-split W2 columns
-      X3 b = wb0, bn = wb1, a[2];
-#pragma unroll
-      for (int t = 0; t < 2; t++)
-#pragma unroll
-        for (int p = 0; p < 3; p++) a[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, 8 * h));
-#pragma unroll
-      for (int s = 0; s < 8; s++) {
-        X3 bnn, an[2];
-        if (s < 6) bnn = WLOAD(1, s + 2);
-        if (s < 7) {
-#pragma unroll
-          for (int t = 0; t < 2; t++)
-#pragma unroll
-            for (int p = 0; p < 3; p++) an[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
-        }
-#pragma unroll
-        for (int t = 0; t < 2; t++) mma3s(a[t], b, dh1[t], dh1s[t]);
-        if (s < 6) X3_PIPE_V(3, 6, 12);
-        else if (s < 7) X3_PIPE(6, 12);
-        X3_SB();
-        if (s < 7) { b = bn; bn = bnn; a[0] = an[0]; a[1] = an[1]; }
-      }
-    }
-#endif
-    LP(7);
-    // dW1 of tile t, k-step s2: registers 8 s2 .. of dh1[t] are the A^T fragment (rows 32t + 16 s2 +
-    // 8(j >> 2) + 4h + (j & 3)); B from the observation image (zeros past feature 15)
-    auto dw1_operands = [&](int t, int s2, X3& a, X3& b) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) v[j] = dh1[t][8 * s2 + j];
-      a = split8(v);
-      const int rr = 32 * t + 16 * s2 + 4 * h + gq;
-#pragma unroll
-      for (int p = 0; p < 3; p++) {
-        const int o0 = ghi ? B_ZERO - B_XO - (rd & 1) * 3 * XIMG + 8 * gp : p * XIMG + rr * XROW + 8 * gp;
-        const int o1 = ghi ? o0 : o0 + 8 * XROW;
-        b.p[p] = cat_tr(rdtr(XO, o0), rdtr(XO, o1));
-      }
-    };
-    // relu'(h1) of tile t from the top piece of the H1 image (h1 >= 0 after the ReLU: its top piece
-    // is > 0 exactly when h1 is a positive normal); register r: row 32t + acc_row(r, h), neuron n_own
-    auto relu_mask = [&](int t) {
-#pragma unroll
-      for (int gg = 0; gg < 4; gg++) {
-        const s16x4 m = rdtr(L + B_H1P, soff(32 * t + 8 * gg + 4 * h + gq, 4 * w + tr_col) + tr_half);
-#pragma unroll
-        for (int q = 0; q < 4; q++) dh1[t][4 * gg + q] = m[q] > 0 ? dh1[t][4 * gg + q] : 0.f;
-      }
-    };
 #if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
-    {  // 16 operand steps (per k-step s: A, then B of jb = 0..3), each read one unit ahead
+    {  // 20 operand blocks (per k-step s: A, then B of jb = 0..3), each read one unit ahead
       // The K order over the rows is free (both operands use it): the 4-row blocks of the transposed
       // reads take rows 4 apart (k-step s, lane half h: element j is row 16s + 2h + (j >> 2) + 4(j & 3)),
       // so a block's rows sit 16 banks apart on the 272-byte rows and a 32-lane half covers the 64
@@ -683,29 +623,10 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       for (int s = 0; s < 4; s++) {
 #pragma unroll
         for (int jb = 0; jb < 4; jb++) {
-          const int it = 4 * s + jb;
           X3 an, bn;
           if (jb < 3) bn = trblk(B_H1P, s, 4 * (jb + 1) + tr_col);
           else if (s < 3) { an = trblk(B_DH2P, s + 1, 4 * w + tr_col); bn = trblk(B_H1P, s + 1, tr_col); }
           dW2[jb] = mma3(a, b, dW2[jb]);
-          // the round's dW1 work, spread over the gaps (two iterations after the last dh1 MFMA issued,
-          // so its drain is covered)
-          if (it == 2) {
-#pragma unroll
-            for (int t = 0; t < 2; t++) dh1[t] += dh1s[t];
-            // the previous round's dW1 into the launch total (round-to-nearest adds; see below)
-            dW1 += dW1b + dW1s;
-#pragma unroll
-            for (int r = 0; r < 16; r++) { dW1b[r] = 0.f; dW1s[r] = 0.f; }
-          }
-          if (it == 3) relu_mask(0);
-          if (it == 8) relu_mask(1);
-          if (it == 4 || it == 6 || it == 10 || it == 12) {
-            const int t = it < 8 ? 0 : 1, s2 = (it == 6 || it == 12) ? 1 : 0;
-            X3 da, db;
-            dw1_operands(t, s2, da, db);
-            mma3s(da, db, dW1b, dW1s);
-          }
           if (jb < 3) X3_PIPE(6, 6);
           else if (s < 3) X3_PIPE(12, 6);
           X3_SB();
@@ -714,16 +635,88 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         }
       }
     }
-#else
-    relu_mask(0);
-    relu_mask(1);
 #endif
+    LP(7);
     LP(8);
+#if !defined(QD_X3_NODH1)
+    // ---- dh1 (R form) = relu'(h1) . (dh2 W2[:, block w]); then the dW1 slab (+ db1 in column 12)
+    f32x16 dh1[2];
+#pragma unroll
+    for (int r = 0; r < 16; r++) { dh1[0][r] = 0.f; dh1[1][r] = 0.f; }
+    f32x16 dh1s[2] = {dh1[0], dh1[1]};
+    {  // software pipeline as L2: A = DH2 row reads, B = pre-split W2 columns
+      X3 b = wb0, bn = wb1, a[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int p = 0; p < 3; p++) a[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, 8 * h));
+#pragma unroll
+      for (int s = 0; s < 8; s++) {
+        X3 bnn, an[2];
+        if (s < 6) bnn = WLOAD(1, s + 2);
+        if (s < 7) {
+#pragma unroll
+          for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int p = 0; p < 3; p++) an[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
+        }
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+#if defined(QD_X3_DH1ONE)
+          dh1[t] = mma3(a[t], b, dh1[t]);
+#else
+          mma3s(a[t], b, dh1[t], dh1s[t]);
+#endif
+        }
+        if (s < 6) X3_PIPE_V(3, 6, 12);
+        else if (s < 7) X3_PIPE(6, 12);
+        X3_SB();
+        if (s < 7) { b = bn; bn = bnn; a[0] = an[0]; a[1] = an[1]; }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 2; t++) dh1[t] += dh1s[t];
     LP(9);
-    // This round's dW1 sits in fresh accumulators (big / small terms), added to the launch total
-    // with round-to-nearest VALU adds one round later (in the next round's dW2 gaps, or after the
-    // last round): one MFMA chain over every row of the block drifted by the truncation bias (mma3s).
-    // Buys first-layer gradients within torch fp32's error (tests/test_gpu_learner.py)
+    // this round's dW1 in fresh accumulators (big / small terms), added to the launch total with
+    // round-to-nearest VALU adds: one MFMA chain over every row of the block drifted by the
+    // truncation bias (mma3s). The previous round's are added here, a round after their MFMAs
+    // issued (no wait on them). Costs ~2.5 % of the launch (the flush's ~130 AGPR moves and adds
+    // per round; flushing every 4th round under a branch spilled); buys first-layer gradients
+    // within torch fp32's error (tests/test_gpu_learner.py)
+    dW1 += dW1b + dW1s;
+#pragma unroll
+    for (int r = 0; r < 16; r++) { dW1b[r] = 0.f; dW1s[r] = 0.f; }
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      f32x16& acc = dh1[t];
+      // register r: row 32t + acc_row(r, h), neuron n_own; relu'(h1) from the top piece of h1
+      // (h1 >= 0 after the ReLU: its top piece is > 0 exactly when h1 is a positive normal)
+#pragma unroll
+      for (int gg = 0; gg < 4; gg++) {
+        const s16x4 m = rdtr(L + B_H1P, soff(32 * t + 8 * gg + 4 * h + gq, 4 * w + tr_col) + tr_half);
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[4 * gg + q] = m[q] > 0 ? acc[4 * gg + q] : 0.f;
+      }
+      // dW1[n][f] += sum_rows dh1[row][n] x[row][f]: registers 8s2.. are the A^T fragment of k-step
+      // s2, rows 32t + 16 s2 + 8(j >> 2) + 4h + (j & 3); B from the observation image (zeros past f 15)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; s2++) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = acc[8 * s2 + j];
+        const X3 a = split8(v);
+        const int rr = 32 * t + 16 * s2 + 4 * h + gq;
+        X3 b;
+#pragma unroll
+        for (int p = 0; p < 3; p++) {
+          const int o0 = ghi ? B_ZERO - B_XO - (rd & 1) * 3 * XIMG + 8 * gp : p * XIMG + rr * XROW + 8 * gp;
+          const int o1 = ghi ? o0 : o0 + 8 * XROW;
+          b.p[p] = cat_tr(rdtr(XO, o0), rdtr(XO, o1));
+        }
+        mma3s(a, b, dW1b, dW1s);
+      }
+    }
+  #endif
     LP(10);
 }
   dW1 += dW1b + dW1s;

@@ -1681,8 +1681,11 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   h->kp.seed = seed;
   h->kp.gid_base = env_id_base;
   // measured on MI355X (DESIGN.md "Step-kernel forms"): the one-thread k_step is fastest while
-  // the batch is about one wave per SIMD; the k_step_g<1> form wins once waves queue up
-  h->lanes = n_envs < (1 << 18) ? 0 : 1;
+  // the batch is about one wave per SIMD; the k_step_g<1> form wins once waves queue up, up to the
+  // batches whose state the 256 MB Infinity Cache holds; past them (true HBM) two lanes per env
+  // (k_step_g<2>: more waves in flight per SIMD) win -- 2M envs 141 vs 152 us, 4M 303 vs 326, 8M
+  // 610 vs 639 (round 4, tools/dram_sweep.py; 1M: 52.8 vs 62.5 the other way)
+  h->lanes = n_envs < (1 << 18) ? 0 : (n_envs <= (1 << 20) ? 1 : 2);
   if (const char* v = std::getenv("QUADENV_LANES")) {
     const int g = std::atoi(v);
     if (g == 0 || g == 1 || g == 2 || g == 4) h->lanes = g;
