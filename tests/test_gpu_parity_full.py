@@ -154,7 +154,7 @@ def test_full_batch_step_matches_oracle(golden_dir, env_name, wrapper, kind, wra
     nterm, ntrunc = int(g["terminated"].sum()), int(g["truncated"].sum())
     print(f"\n{env_name}/{wrapper} spec {spec_mode}: {N_FULL} rows, {ng} golden, terminated {nterm}, "
           f"truncated {ntrunc}, operand-relative-only components {slack}")
-    assert nterm > 1000 and ntrunc > 1000  # the case exercised both flags
+    assert nterm > 300 and ntrunc > 1000  # the case exercised both flags (measured 424 .. 1,500 terminations)
     env.close()
 
 

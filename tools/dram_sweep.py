@@ -12,7 +12,9 @@ import torch  # noqa: E402
 
 
 def point(n, lanes, launches):
-    os.environ["QUADENV_LANES"] = str(lanes)
+    # lanes: 1 / 2 / 4 = k_step_g<G>; "0" = k_step_h (helper waves); "0n" = k_step (one thread per env)
+    os.environ["QUADENV_LANES"] = str(lanes)[0]
+    os.environ["QUADENV_HELPER"] = "0" if str(lanes).endswith("n") else "1"
     from uav_reinforcement_learning_control_amd import _native as N
     if os.environ.get("QUADENV_LIB"):  # an A/B build (tools/probe/build_variant.sh)
         N.LIB_PATH = os.environ["QUADENV_LIB"]
@@ -35,7 +37,7 @@ def point(n, lanes, launches):
 if __name__ == "__main__":
     sizes = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else \
         [1 << 18, 1 << 19, 1 << 20, 1 << 21, 1 << 22, 1 << 23]
-    lanes_list = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 4]
+    lanes_list = sys.argv[2].split(",") if len(sys.argv) > 2 else ["1", "2", "4"]
     for n in sizes:
         for lanes in lanes_list:
             launches = 200 if n <= (1 << 20) else 100 if n <= (1 << 22) else 100

@@ -10,8 +10,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-VARIANTS = [("base", "2"), ("base", "1"), ("NOENV", "2"), ("NOMLP", "2"), ("NOCRITIC", "2"),
-            ("NOENV", "1"), ("NOMLP", "1")]
+VARIANTS = [("base", "2"), ("OVL0", "2"), ("PK0", "2"), ("base", "2"), ("OVL0", "2"), ("PK0", "2"),
+            ("NOENV", "2"), ("NOMLP", "2"), ("NOCRITIC", "2"), ("base", "1")]
 
 
 def main():

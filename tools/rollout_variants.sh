@@ -1,17 +1,23 @@
 #!/bin/bash
 # Profiling tool (not product): cost-ablation builds of libquadenv.so for tools/rollout_variants.py --
-# k_rollout without the env step, without the MLPs, without the critic. Output: tools/_build/roll_*.so
+# k_rollout without the env step, without the MLPs, without the critic, and the round-3 order (OVL0).
+# Output: tools/_build/roll_*.so
+# (the other objects from the in-tree build)
 set -e
 cd "$(dirname "$0")/../uav_reinforcement_learning_control_amd/csrc"
+make -s
 mkdir -p ../../tools/_build/obj
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on"
-/opt/rocm/bin/hipcc $F -fno-slp-vectorize -c -o ../../tools/_build/obj/quadenv.o quadenv.hip &
-/opt/rocm/bin/hipcc $F -c -o ../../tools/_build/obj/policy.o policy.hip &
+O=../_lib/obj
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -ffp-contract=on -I$O"
 for v in NOENV NOMLP NOCRITIC; do
   /opt/rocm/bin/hipcc $F -fno-slp-vectorize -DQD_ROLL_$v -c -o ../../tools/_build/obj/rollout_$v.o rollout.hip &
 done
+# OVL0: the round-3 order (env step after both nets) for the A/B of the overlapped form
+/opt/rocm/bin/hipcc $F -fno-slp-vectorize -DQD_ROLL_OVL=0 -c -o ../../tools/_build/obj/rollout_OVL0.o rollout.hip &
+# PK0: the actor head on four v_fma_f32 per hidden value instead of two v_pk_fma_f32
+/opt/rocm/bin/hipcc $F -fno-slp-vectorize -DQD_HEAD_PK=0 -c -o ../../tools/_build/obj/rollout_PK0.o rollout.hip &
 wait
-for v in NOENV NOMLP NOCRITIC; do
+for v in NOENV NOMLP NOCRITIC OVL0 PK0; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/_build/roll_$v.so \
-    ../../tools/_build/obj/quadenv.o ../../tools/_build/obj/policy.o ../../tools/_build/obj/rollout_$v.o
+    $O/quadenv.o $O/policy.o ../../tools/_build/obj/rollout_$v.o $O/learner.o $O/learner_x3.o
 done

@@ -124,6 +124,14 @@ static_assert(2 * LB * 8 <= 3 * IMG, "the advantage reduction aliases the DH2 im
 
 __device__ __forceinline__ int soff(int row, int ch) { return RS * row + 16 * ch; }
 
+// QD_X3_PK: the actor's head partial sums and dW3 accumulations as v_pk_fma_f32 pairs (each lane of
+// a packed FMA is the same fused multiply-add: the same bits, tools/x3_bits_ab.py). Measured
+// (round 4): 778.8 / 778.3 us vs 775.6 / 767.2 with single FMAs -- the register pairs the packed
+// operands need raise the spills 8 -> 15; default off
+#ifndef QD_X3_PK
+#define QD_X3_PK 0
+#endif
+
 // three-piece split of two floats (exact residuals: x - bf16(x) is representable in f32)
 __device__ __forceinline__ void split2(float a, float b, bf16x2& p0, bf16x2& p1, bf16x2& p2) {
   const f32x2 x = {a, b};
@@ -513,8 +521,16 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         h2[t][r] = relu(h2[t][r]);
         const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * (32 * w + acc_row(r, h)));
         const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
+        if constexpr (NOUT == ACT && QD_X3_PK) {  // two v_pk_fma_f32: the same four fmas
+          const f32x2 hh = {h2[t][r], h2[t][r]};
+          f32x2 p01 = {part[0], part[1]}, p23 = {part[2], part[3]};
+          p01 = __builtin_elementwise_fma(f32x2{wk[0], wk[1]}, hh, p01);
+          p23 = __builtin_elementwise_fma(f32x2{wk[2], wk[3]}, hh, p23);
+          part[0] = p01[0]; part[1] = p01[1]; part[2] = p23[0]; part[3] = p23[1];
+        } else {
 #pragma unroll
-        for (int k = 0; k < NOUT; k++) part[k] = fmaf(wk[k], h2[t][r], part[k]);
+          for (int k = 0; k < NOUT; k++) part[k] = fmaf(wk[k], h2[t][r], part[k]);
+        }
       }
 #pragma unroll
       for (int k = 0; k < NOUT; k++) {
@@ -587,8 +603,16 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
           for (int k = 0; k < NOUT; k++) gsum = fmaf(wk[k], d[t][k], gsum);
           v[u] = h2[t][r] > 0.f ? gsum : 0.f;
+          if constexpr (NOUT == ACT && QD_X3_PK) {  // two v_pk_fma_f32: the same four fmas
+            const f32x2 hh = {h2[t][r], h2[t][r]};
+            f32x2 a01 = {dW3[0][r], dW3[1][r]}, a23 = {dW3[2][r], dW3[3][r]};
+            a01 = __builtin_elementwise_fma(f32x2{d[t][0], d[t][1]}, hh, a01);
+            a23 = __builtin_elementwise_fma(f32x2{d[t][2], d[t][3]}, hh, a23);
+            dW3[0][r] = a01[0]; dW3[1][r] = a01[1]; dW3[2][r] = a23[0]; dW3[3][r] = a23[1];
+          } else {
 #pragma unroll
-          for (int k = 0; k < NOUT; k++) dW3[k][r] = fmaf(d[t][k], h2[t][r], dW3[k][r]);  // h2: relu'd
+            for (int k = 0; k < NOUT; k++) dW3[k][r] = fmaf(d[t][k], h2[t][r], dW3[k][r]);  // h2: relu'd
+          }
           dB2[r] += v[u];
         }
         const X3h x = split4(v);

@@ -81,6 +81,12 @@ __device__ __forceinline__ void bias_init(f32x16& acc, const float* L, int off) 
 // 1/16 of one 32-neuron block's head: ReLU of accumulator register(s) `i` (actor: register i; critic:
 // registers 4(i/4).. handled at i % 4 == 0) times the packed head weights, into part[][].
 // (o3 = NET_W3 + 4h: the lane's part of the head-weight region)
+// QD_HEAD_PK: the actor head's four FMAs per hidden value as two v_pk_fma_f32 (each lane of a
+// packed FMA is the same fused multiply-add, so the same bits, tools/env_digest.py); 0 = four
+// v_fma_f32. Round 4 A/B (k_rollout, 65,536 envs): 27.63 / 27.74 vs 27.73 / 27.93 us per step
+#ifndef QD_HEAD_PK
+#define QD_HEAD_PK 1
+#endif
 template <int NOUT, int NT>
 __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32x16 (&x)[NT], int m, int i,
                                           int o3, float (&part)[NT][NOUT]) {
@@ -89,10 +95,18 @@ __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32
 #pragma unroll
     for (int j = 0; j < NT; j++) {
       const float v = relu(x[j][i]);
+#if QD_HEAD_PK
+      const f32x2 vv = {v, v}, w01 = {w.x, w.y}, w23 = {w.z, w.w};
+      f32x2 p01 = {part[j][0], part[j][1]}, p23 = {part[j][2], part[j][3]};
+      p01 = __builtin_elementwise_fma(w01, vv, p01);
+      p23 = __builtin_elementwise_fma(w23, vv, p23);
+      part[j][0] = p01[0]; part[j][1] = p01[1]; part[j][2] = p23[0]; part[j][3] = p23[1];
+#else
       part[j][0] = fmaf(w.x, v, part[j][0]);
       part[j][1] = fmaf(w.y, v, part[j][1]);
       part[j][2] = fmaf(w.z, v, part[j][2]);
       part[j][3] = fmaf(w.w, v, part[j][3]);
+#endif
     }
   } else {
     if (i % 4 != 0) return;
@@ -256,11 +270,19 @@ __device__ __forceinline__ void pipe_start(const float* __restrict__ L, const Ne
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// a caller's work for the issue gaps of layer-2 step g (none by default): called inside step g's
+// scheduling region, so its VALU interleaves with that step's MFMAs (the fused rollout hangs the env
+// step on the critic's steps, rollout.hip)
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
 // one net's 32 layer-2 steps (+ layer 1 of its blocks 1..3, and with NEXT the next net's block 0
 // and first fragments), then its head
-template <int NOUT, int NT, bool NEXT, int G0>
+template <int NOUT, int NT, bool NEXT, int G0, typename Hook = NoHook>
 __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetOff& o, const NetOff& on,
-                                         const P3 (&xp)[NT], Pipe<NT>& st, float (&out)[NT][NOUT]) {
+                                         const P3 (&xp)[NT], Pipe<NT>& st, float (&out)[NT][NOUT],
+                                         Hook&& hook = Hook{}) {
   const int h = (threadIdx.x >> 5) & 1;
   f32x16 acc[4][NT];
 #pragma unroll
@@ -300,6 +322,7 @@ __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetO
           split_pair(relu(a1n[j][8 * tt + 2 * k]), relu(a1n[j][8 * tt + 2 * k + 1]), st.h1[nb][j][tt], k);
         }
       }
+      hook(g);
 #if QD_NF_VPG > 0
 #pragma unroll
       for (int q = 0; q < 6 * NT; q++) {

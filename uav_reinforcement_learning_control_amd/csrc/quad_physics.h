@@ -384,16 +384,24 @@ struct ForceAcc {
   T FB[3], tau[3], Qs[4];
 };
 
+// forward_base in pieces (same operations in the same order, so the same bits): the rotation, the
+// base-frame velocity, gravity and the base drag; then each prop's drag, accumulated in prop order.
+// The fused rollout spreads the pieces over the critic's MFMA issue gaps (rollout.hip).
 template <typename T>
-QD_HD void forward_base(const PhysConsts<T>& c, const T qn[4], const T th[4], const T v[3], const T w[3],
-                        const T s[4], ForceAcc<T>& o) {
+struct BaseAcc {
+  ForceAcc<T> a;
+  T vB[3];
+};
+template <typename T>
+QD_HD void forward_base_begin(const PhysConsts<T>& c, const T qn[4], const T v[3], const T w[3], BaseAcc<T>& b) {
+  ForceAcc<T>& o = b.a;
   // R = quat2mat(q) (q already normalized)
   const T qw = qn[0], qx = qn[1], qy = qn[2], qz = qn[3];
   T* R = o.R;
   R[0] = T(1) - T(2) * (qy * qy + qz * qz); R[1] = T(2) * (qx * qy - qw * qz); R[2] = T(2) * (qx * qz + qw * qy);
   R[3] = T(2) * (qx * qy + qw * qz); R[4] = T(1) - T(2) * (qx * qx + qz * qz); R[5] = T(2) * (qy * qz - qw * qx);
   R[6] = T(2) * (qx * qz - qw * qy); R[7] = T(2) * (qy * qz + qw * qx); R[8] = T(1) - T(2) * (qx * qx + qy * qy);
-  T vB[3];
+  T* vB = b.vB;
 #pragma unroll
   for (int i = 0; i < 3; i++) vB[i] = R[i] * v[0] + R[3 + i] * v[1] + R[6 + i] * v[2];
   T* FB = o.FB;
@@ -413,34 +421,46 @@ QD_HD void forward_base(const PhysConsts<T>& c, const T qn[4], const T th[4], co
 #pragma unroll
     for (int i = 0; i < 3; i++) { FB[i] += f[i]; tau[i] += t[i]; }
   }
-  // prop fluid: prop frame = base frame rotated by th_i about z; COM on the axis at pc_i
-  // (written as explicit fma chains: -ffp-contract=on fuses only within one expression, and the
-  // cross products, frame rotations and accumulations below are ~1/3 of the physics)
-  T* Qs = o.Qs;
+}
+// prop fluid: prop frame = base frame rotated by th_p about z; COM on the axis at pc_p
+// (written as explicit fma chains: -ffp-contract=on fuses only within one expression, and the
+// cross products, frame rotations and accumulations below are ~1/3 of the physics)
+template <typename T>
+QD_HD void forward_prop(const PhysConsts<T>& c, int p, T th, const T w[3], T s, BaseAcc<T>& b) {
+  T* FB = b.a.FB;
+  T* tau = b.a.tau;
+  const T* vB = b.vB;
+  T sn, cs;
+  prop_sincos(th, &sn, &cs);
+  const T* r = c.pc[p];
+  const T ub[3] = {q_fma(w[1], r[2], q_fma(-w[2], r[1], vB[0])),  // vB + w x r
+                   q_fma(w[2], r[0], q_fma(-w[0], r[2], vB[1])),
+                   q_fma(w[0], r[1], q_fma(-w[1], r[0], vB[2]))};
+  const T wp[3] = {q_fma(cs, w[0], sn * w[1]), q_fma(-sn, w[0], cs * w[1]), w[2] + s};
+  const T up[3] = {q_fma(cs, ub[0], sn * ub[1]), q_fma(-sn, ub[0], cs * ub[1]), ub[2]};
+  T tp[3], fp[3];
+  box_drag(wp, up, c.p_kqa, c.p_kva, c.p_kql, c.p_kvl, tp, fp);
+  const T f[3] = {q_fma(cs, fp[0], -sn * fp[1]), q_fma(sn, fp[0], cs * fp[1]), fp[2]};  // back to base
+  FB[0] += f[0]; FB[1] += f[1]; FB[2] += f[2];
+  // tau += r x f + Rz(th) tp
+  tau[0] = q_fma(r[1], f[2], q_fma(-r[2], f[1], q_fma(cs, tp[0], q_fma(-sn, tp[1], tau[0]))));
+  tau[1] = q_fma(r[2], f[0], q_fma(-r[0], f[2], q_fma(sn, tp[0], q_fma(cs, tp[1], tau[1]))));
+  tau[2] = q_fma(r[0], f[1], q_fma(-r[1], f[0], tau[2] + tp[2]));
+  b.a.Qs[p] = tp[2];
+}
+
+template <typename T>
+QD_HD void forward_base(const PhysConsts<T>& c, const T qn[4], const T th[4], const T v[3], const T w[3],
+                        const T s[4], ForceAcc<T>& o) {
+  BaseAcc<T> b;
+  forward_base_begin(c, qn, v, w, b);
 #if defined(QD_ABL_NOPROPS)  // cost ablation (tools only): no prop drag terms
-  Qs[0] = Qs[1] = Qs[2] = Qs[3] = T(0);
+  b.a.Qs[0] = b.a.Qs[1] = b.a.Qs[2] = b.a.Qs[3] = T(0);
   if (false)
 #endif
 #pragma unroll
-  for (int p = 0; p < 4; p++) {
-    T sn, cs;
-    prop_sincos(th[p], &sn, &cs);
-    const T* r = c.pc[p];
-    const T ub[3] = {q_fma(w[1], r[2], q_fma(-w[2], r[1], vB[0])),  // vB + w x r
-                     q_fma(w[2], r[0], q_fma(-w[0], r[2], vB[1])),
-                     q_fma(w[0], r[1], q_fma(-w[1], r[0], vB[2]))};
-    const T wp[3] = {q_fma(cs, w[0], sn * w[1]), q_fma(-sn, w[0], cs * w[1]), w[2] + s[p]};
-    const T up[3] = {q_fma(cs, ub[0], sn * ub[1]), q_fma(-sn, ub[0], cs * ub[1]), ub[2]};
-    T tp[3], fp[3];
-    box_drag(wp, up, c.p_kqa, c.p_kva, c.p_kql, c.p_kvl, tp, fp);
-    const T f[3] = {q_fma(cs, fp[0], -sn * fp[1]), q_fma(sn, fp[0], cs * fp[1]), fp[2]};  // back to base
-    FB[0] += f[0]; FB[1] += f[1]; FB[2] += f[2];
-    // tau += r x f + Rz(th) tp
-    tau[0] = q_fma(r[1], f[2], q_fma(-r[2], f[1], q_fma(cs, tp[0], q_fma(-sn, tp[1], tau[0]))));
-    tau[1] = q_fma(r[2], f[0], q_fma(-r[0], f[2], q_fma(sn, tp[0], q_fma(cs, tp[1], tau[1]))));
-    tau[2] = q_fma(r[0], f[1], q_fma(-r[1], f[0], tau[2] + tp[2]));
-    Qs[p] = tp[2];
-  }
+  for (int p = 0; p < 4; p++) forward_prop(c, p, th[p], w, s[p], b);
+  o = b.a;
 }
 
 // The motor wrench of mj_fwdActuation for ctrl F (site transmission; float64 -> T): total thrust
