@@ -10,8 +10,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-VARIANTS = [("base", "2"), ("OVL0", "2"), ("PK0", "2"), ("base", "2"), ("OVL0", "2"), ("PK0", "2"),
-            ("NOENV", "2"), ("NOMLP", "2"), ("NOCRITIC", "2"), ("base", "1")]
+VARIANTS = [("base", "2"), ("ALP0", "2"), ("base", "2"), ("ALP0", "2"), ("base", "2"), ("ALP0", "2"),
+            ("NOENV", "2"), ("NOMLP", "2"), ("NOCRITIC", "2")]
 
 
 def main():

@@ -187,7 +187,16 @@ struct NetOff {
   int w1, w2, b, w3;
   gbf16x8* wp;   // this net's pre-split W2 pieces, this lane's unit
   gbf16x8* w1p;  // and W1's
+  int lpa, lpb;  // LDS byte offsets of this lane's unit of the actor's W2 pieces (stage_pieces)
 };
+// The actor's pre-split W2 pieces in LDS (k_rollout: staged once per launch, read by ds_read_b128
+// instead of three global loads per k-step): the f32 W2 regions of the image are not staged since
+// round 3, so the 96 KB go into the actor's (k-steps 0 .. LP_SPLIT - 1, 3 KB each) and the
+// critic's (the rest). The critic's pieces stay in L2 (both nets' would be 192 KB).
+constexpr int LP_SPLIT = 21;
+constexpr int LP_A = NET_W2 * 4, LP_B = (ACTOR_F + NET_W2) * 4;
+static_assert(LP_SPLIT * 3072 <= W2_F * 4 && (32 - LP_SPLIT) * 3072 <= W2_F * 4, "pieces fit the W2 regions");
+static_assert(LP_A % 16 == 0 && LP_B % 16 == 0, "16-byte aligned LDS pieces");
 // `packed`: the global packed image; its scalar base is made opaque per call, so the compiler
 // cannot hoist the pieces' loads out of the callers' step loops (hundreds of VGPRs)
 __device__ __forceinline__ NetOff net_off(int base, const float* packed, int net) {
@@ -196,8 +205,9 @@ __device__ __forceinline__ NetOff net_off(int base, const float* packed, int net
   asm volatile("" : "+s"(pb));
   NetOff o{base + NET_W1 + lane * 8, base + NET_W2 + lane * 8, base + NET_B1 + h * 16, base + NET_W3 + h * 4,
            reinterpret_cast<gbf16x8*>(pb) + net * (32 * 3 * 64) + lane,
-           reinterpret_cast<gbf16x8*>(pb) + 2 * (32 * 3 * 64) + net * (4 * 3 * 64) + lane};
-  asm volatile("" : "+v"(o.w1), "+v"(o.w2), "+v"(o.b), "+v"(o.w3));
+           reinterpret_cast<gbf16x8*>(pb) + 2 * (32 * 3 * 64) + net * (4 * 3 * 64) + lane,
+           LP_A + lane * 16, LP_B + lane * 16};
+  asm volatile("" : "+v"(o.w1), "+v"(o.w2), "+v"(o.b), "+v"(o.w3), "+v"(o.lpa), "+v"(o.lpb));
   return o;
 }
 // the pre-split W1 fragment of layer-1 block n (k_policy_pack; the same pieces as ld_split8 of the
@@ -208,11 +218,21 @@ __device__ __forceinline__ P3 w1_pieces(const NetOff& o, int n) {
   for (int p = 0; p < 3; p++) x.p[p] = o.w1p[(n * 3 + p) * 64];
   return x;
 }
-// the pre-split W2 fragment of layer-2 k-step g (three dwordx4 loads)
-__device__ __forceinline__ P3 w2_pieces(const NetOff& o, int g) {
+// the pre-split W2 fragment of layer-2 k-step g (three dwordx4 loads; LP: three ds_read_b128 of
+// the actor's pieces staged in LDS)
+template <bool LP = false>
+__device__ __forceinline__ P3 w2_pieces(const float* L, const NetOff& o, int g) {
   P3 x;
+  if constexpr (LP) {
+    const char* Lc = reinterpret_cast<const char*>(L);
 #pragma unroll
-  for (int p = 0; p < 3; p++) x.p[p] = o.wp[(g * 3 + p) * 64];
+    for (int p = 0; p < 3; p++)
+      x.p[p] = *reinterpret_cast<const bf16x8*>(Lc + (g < LP_SPLIT ? o.lpa + (g * 3 + p) * 1024
+                                                                   : o.lpb + ((g - LP_SPLIT) * 3 + p) * 1024));
+  } else {
+#pragma unroll
+    for (int p = 0; p < 3; p++) x.p[p] = o.wp[(g * 3 + p) * 64];
+  }
   return x;
 }
 // W2 fragment of layer-2 k-step g = 8n + 4t + m
@@ -250,7 +270,7 @@ struct Pipe {
 };
 
 // block 0 of a net before its pipeline starts (the first net of a call)
-template <int NT>
+template <int NT, bool LP = false>
 __device__ __forceinline__ void pipe_start(const float* __restrict__ L, const NetOff& o, const P3 (&xp)[NT],
                                            Pipe<NT>& st) {
   f32x16 b;
@@ -265,8 +285,8 @@ __device__ __forceinline__ void pipe_start(const float* __restrict__ L, const Ne
       for (int k = 0; k < 4; k++)
         split_pair(relu(a1[8 * t + 2 * k]), relu(a1[8 * t + 2 * k + 1]), st.h1[0][j][t], k);
   }
-  st.wr[0] = w2_pieces(o, 0);
-  st.wr[1] = w2_pieces(o, 1);
+  st.wr[0] = w2_pieces<LP>(L, o, 0);
+  st.wr[1] = w2_pieces<LP>(L, o, 1);
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -279,7 +299,8 @@ struct NoHook {
 
 // one net's 32 layer-2 steps (+ layer 1 of its blocks 1..3, and with NEXT the next net's block 0
 // and first fragments), then its head
-template <int NOUT, int NT, bool NEXT, int G0, typename Hook = NoHook>
+// (LP: this net's W2 pieces come from LDS -- the actor in k_rollout; the next net's always from L2)
+template <int NOUT, int NT, bool NEXT, int G0, bool LP = false, typename Hook = NoHook>
 __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetOff& o, const NetOff& on,
                                          const P3 (&xp)[NT], Pipe<NT>& st, float (&out)[NT][NOUT],
                                          Hook&& hook = Hook{}) {
@@ -303,7 +324,7 @@ __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetO
     for (int s = 0; s < 8; s++) {
       const int g = 8 * n + s, t = s >> 2, m = s & 3;
       if (g + 2 < 32 || NEXT)  // step g + 2's pieces into the ring slot step g - 1 freed
-        st.wr[(G0 + g + 2) % 3] = g + 2 < 32 ? w2_pieces(o, g + 2) : w2_pieces(on, g + 2 - 32);
+        st.wr[(G0 + g + 2) % 3] = g + 2 < 32 ? w2_pieces<LP>(L, o, g + 2) : w2_pieces(L, on, g + 2 - 32);
 #pragma unroll
       for (int j = 0; j < NT; j++) acc[m][j] = mfma6(st.wr[(G0 + g) % 3], st.h1[cb][j][t].p(), acc[m][j]);
       if (pre && s == 1) {
@@ -369,7 +390,8 @@ __device__ __forceinline__ void net_forward(const float* __restrict__ L, const f
 
 // actor (image at L) then critic (at L + ACTOR_F) in one pipeline: the same bits as two net_forward
 // calls (every tile's operations and their order are the same)
-template <int NT>
+// (ALP: the actor's W2 pieces from LDS, staged by stage_pieces)
+template <int NT, bool ALP = false>
 __device__ __forceinline__ void net_forward2(const float* __restrict__ L, const float* packed, const float (&xq)[NT][8],
                                              float (&mean)[NT][ACT], float (&val)[NT][1]) {
   P3 xp[NT];
@@ -377,8 +399,8 @@ __device__ __forceinline__ void net_forward2(const float* __restrict__ L, const 
   for (int j = 0; j < NT; j++) xp[j] = split8(xq[j]);
   const NetOff oa = net_off(0, packed, 0), oc = net_off(ACTOR_F, packed, 1);
   Pipe<NT> st;
-  pipe_start<NT>(L, oa, xp, st);
-  net_core<ACT, NT, true, 0>(L, oa, oc, xp, st, mean);
+  pipe_start<NT, ALP>(L, oa, xp, st);
+  net_core<ACT, NT, true, 0, ALP>(L, oa, oc, xp, st, mean);
   net_core<1, NT, false, 32>(L, oc, oc, xp, st, val);
 }
 
@@ -409,6 +431,29 @@ __device__ __forceinline__ void stage_lds(float* lds, const float* __restrict__ 
     for (int j = 0; j < BATCH; j++) {
       const int k = (b0 + j) * BLK + threadIdx.x;
       if (b0 + j < PER && k < NV) dst[stage_map(k)] = v[j];
+    }
+  }
+  __syncthreads();
+}
+
+// the actor's 96 KB of pre-split W2 pieces (global [k-step][piece][lane] units of 16 bytes, right
+// after the packed image) into the LDS regions LP_A / LP_B (see LP_SPLIT); ends with a barrier
+template <int BLK>
+__device__ __forceinline__ void stage_pieces(float* lds, const float* __restrict__ packed) {
+  constexpr int NV = 32 * 3 * 64, PER = NV / BLK, BATCH = PER % 8 == 0 ? 8 : 4;
+  static_assert(NV % BLK == 0 && PER % BATCH == 0, "whole batches");
+  const float4* src = reinterpret_cast<const float4*>(packed + PACKED_F);
+  char* Lc = reinterpret_cast<char*>(lds);
+#pragma unroll
+  for (int b0 = 0; b0 < PER; b0 += BATCH) {
+    float4 v[BATCH];
+#pragma unroll
+    for (int j = 0; j < BATCH; j++) v[j] = src[(b0 + j) * BLK + threadIdx.x];
+#pragma unroll
+    for (int j = 0; j < BATCH; j++) {
+      const int u = (b0 + j) * BLK + int(threadIdx.x), g = u / 192;  // unit (g, p, lane) = (g * 3 + p) * 64 + lane
+      const int off = g < LP_SPLIT ? LP_A + u * 16 : LP_B + (u - LP_SPLIT * 192) * 16;
+      *reinterpret_cast<float4*>(Lc + off) = v[j];
     }
   }
   __syncthreads();

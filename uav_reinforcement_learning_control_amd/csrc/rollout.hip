@@ -115,6 +115,11 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, size_t row, 
 #ifndef QD_ROLL_OVL
 #define QD_ROLL_OVL 0
 #endif
+// QD_ROLL_ALP: the actor's W2 pieces from LDS (policy_net.h stage_pieces / LP_SPLIT), the
+// critic's from L2; 0 = both from L2 (round 3). Same bits.
+#ifndef QD_ROLL_ALP
+#define QD_ROLL_ALP 1
+#endif
 
 // the Gaussian action of this lane's env (SB3 policy.forward: a = mean + std z), its log-prob as
 // PPO.train recomputes it, and the clipped action the env receives
@@ -214,6 +219,9 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
   }
   float ls = a.last_start[i], ret = a.ep_ret[i], len = a.ep_len[i];
   stage_lds<BLK>(lds, packed);
+#if QD_ROLL_ALP
+  stage_pieces<BLK>(lds, packed);  // the actor's W2 pieces, once per launch
+#endif
   const float* log_std = packed + LDS_F;
   float lstd[ACT], sd[ACT];
 #pragma unroll
@@ -245,8 +253,8 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
       for (int j = 0; j < NT; j++) xp[j] = split8(xb[j]);
       const NetOff oa = net_off(0, packed, 0), oc = net_off(ACTOR_F, packed, 1);
       Pipe<NT> pst;
-      pipe_start<NT>(lds, oa, xp, pst);
-      net_core<ACT, NT, true, 0>(lds, oa, oc, xp, pst, mean);
+      pipe_start<NT, bool(QD_ROLL_ALP)>(lds, oa, xp, pst);
+      net_core<ACT, NT, true, 0, bool(QD_ROLL_ALP)>(lds, oa, oc, xp, pst, mean);
       sample_action<NT>(a, p, i, t, h, mean, sd, lstd, act, ac, lp);
       StepCo<CTBR> co;
       net_core<1, NT, false, 32>(lds, oc, oc, xp, pst, val, [&](int g) { co.chunk(K, e, ac, r, g); });
@@ -264,7 +272,7 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
 #pragma unroll
     for (int j = 0; j < NT; j++) val[j][0] = mean[j][0];
 #else
-    net_forward2<NT>(lds, packed, xb, mean, val);
+    net_forward2<NT, bool(QD_ROLL_ALP)>(lds, packed, xb, mean, val);
 #endif
 #endif
 #if defined(QD_ROLL_NOMLP) || !QD_ROLL_OVL
