@@ -93,6 +93,29 @@ def _gated_kernel_us(step, actions, n_launch: int = 200) -> float:
     return e0.elapsed_time(e1) * 1e3 / (max(1, n_launch // chunk) * chunk)
 
 
+def _launch_floor_us(n_launch: int = 400) -> float:
+    """Device time per launch of an (almost) empty kernel graph-replayed back to back on the
+    current stream, timed like _gated_kernel_us: the dispatch floor every one-launch step pays
+    whatever it does (1.61-1.63 us on MI355X for any grid from 64 x 128 to 2048 x 64 threads,
+    tools/diag/launch_floor.hip, profiles/r04/r4_launch_floor.txt)."""
+    chunk = 100
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(chunk):
+            torch.cuda._sleep(0)
+    _graph_upload(g)
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda._sleep(200_000)
+    e0.record()
+    for _ in range(max(1, n_launch // chunk)):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (max(1, n_launch // chunk) * chunk)
+
+
 def _kernel_name(env) -> str:
     """The step kernel form the handle actually launches (quad_kernel_form: lanes | 16 SPEC | 32 helper)."""
     from uav_reinforcement_learning_control_amd import _native as N
@@ -170,7 +193,7 @@ def _run_rank(args, rank, world, local_rank):
     # per-launch kernel time (roofline) on the same kernel, stream and data
     res = dict(elapsed=elapsed, region_us=region_us,
                kernel_us=_gated_kernel_us(step, actions, args.kernel_launches),
-               kernel=_kernel_name(env), symbol=_kernel_symbol(env))
+               kernel=_kernel_name(env), symbol=_kernel_symbol(env), launch_floor_us=_launch_floor_us())
     if args.rollout_steps > 0:
         res["rollout"] = _rollout_phase(env, args)
     if args.e2e_iters > 0:
@@ -654,6 +677,21 @@ def _check_launch(args, rank: int, world: int) -> None:
                           "global_envs": args.envs * world}), flush=True)
 
 
+def _launch_terms(res, envs: int) -> dict:
+    """The one-launch step against its dispatch floor: the HBM fraction of the time beyond the
+    empty-kernel launch cost, and the ceiling a one-launch step of these bytes could reach (a
+    zero-latency kernel moving them at the peak: bytes / peak / (bytes / peak + floor))."""
+    fl = res.get("launch_floor_us")
+    if not fl:
+        return {}
+    byt = BYTES_PER_ENV_STEP * envs
+    at_peak_us = byt / (HBM_PEAK_GBS * 1e3)
+    beyond = res["kernel_us"] - fl
+    return {"launch_floor_us": fl,
+            "frac_beyond_launch_floor": (byt / (beyond * 1e-6) / 1e9) / HBM_PEAK_GBS if beyond > 0 else None,
+            "frac_ceiling_one_launch": at_peak_us / (at_peak_us + fl)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -730,7 +768,7 @@ def main():
                      "traffic": traffic["bytes_per_launch"] if traffic else None, "traffic_pmc": traffic,
                      "kernel": res["kernel"], "kernel_symbol": res["symbol"], "kernel_us": kus,
                      "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs,
-                     "issue": _pmc_issue(res["symbol"], args.envs)},
+                     "issue": _pmc_issue(res["symbol"], args.envs), **_launch_terms(res, args.envs)},
     }
     if "rollout" in res:
         line["rollout_phase"] = res["rollout"]

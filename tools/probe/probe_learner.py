@@ -2,8 +2,9 @@
 """Profiling tool (not product): where a k_ppo_grad_x3 round's time goes, from the QD_LPROBE build
 (tools/probe/build_learner_probe.sh -> tools/_build/lprobe.so): per-wave s_memtime stamps of round 2
 of every block, recorded through the dump build's buffer (quad_ppo_hidden). Phases:
-  0-1 obs image + B1 | 1-2 L1 + H1 image + B2 | 2-3 L2 MFMAs | 3-4 head partials + B3 |
-  4-5 loss terms | 5-6 dh2 + images + B4 | 6-7 dW2 (+ db2) | 7-8 dW3 | 8-9 dh1 MFMAs | 9-10 relu' + dW1
+  0-1 obs image + B1 | 1-2 L1 + H1 image | 2-3 wait at B2 | 3-4 L2 MFMAs | 4-5 head partials |
+  5-6 wait at B3 | 6-7 loss terms | 7-8 dh2 + images | 8-9 wait at B4 | 9-10 dW2 (+ db2) |
+  10-11 dh1 MFMAs | 11-12 relu' + dW1 (to the next round's start)
 Usage: probe_learner.py [B]"""
 import os
 import sys
@@ -32,8 +33,8 @@ def main():
     idx = torch.randperm(M, device="cuda")[:B].contiguous()
     L = FusedLearner(pol, 0.2, 0.0, 0.5)
     hidden = torch.zeros(2, B, 256, device="cuda")
-    names = ["obs image + B1", "L1 + H1 image + B2", "L2 MFMAs", "head partials + B3", "loss terms",
-             "dh2 + images + B4", "dW2 (+ db2)", "dW3", "dh1 MFMAs", "relu' + dW1"]
+    names = ["obs image + B1", "L1 + H1 image", "wait at B2", "L2 MFMAs", "head partials", "wait at B3",
+             "loss terms", "dh2 + images", "wait at B4", "dW2 (+ db2)", "dh1 MFMAs", "relu' + dW1"]
     for rep in range(3):
         L.grads(obs, act, lp, adv, ret, idx, hidden=hidden)
         torch.cuda.synchronize()
@@ -43,7 +44,7 @@ def main():
         a = st[st[:, 15] == nout].astype(np.float64)
         if len(a) == 0:
             continue
-        tot = a[:, 10] - a[:, 0]
+        tot = a[:, 12] - a[:, 0]
         print(f"{nm}: {len(a)} waves; round 2 median {np.median(tot):.0f} cycles (p10 {np.percentile(tot, 10):.0f}, "
               f"p90 {np.percentile(tot, 90):.0f})")
         for k, n in enumerate(names):

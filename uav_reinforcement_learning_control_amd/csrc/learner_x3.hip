@@ -124,14 +124,6 @@ static_assert(2 * LB * 8 <= 3 * IMG, "the advantage reduction aliases the DH2 im
 
 __device__ __forceinline__ int soff(int row, int ch) { return RS * row + 16 * ch; }
 
-// QD_X3_PK: the actor's head partial sums and dW3 accumulations as v_pk_fma_f32 pairs (each lane of
-// a packed FMA is the same fused multiply-add: the same bits, tools/x3_bits_ab.py). Measured
-// (round 4): 778.8 / 778.3 us vs 775.6 / 767.2 with single FMAs -- the register pairs the packed
-// operands need raise the spills 8 -> 15; default off
-#ifndef QD_X3_PK
-#define QD_X3_PK 0
-#endif
-
 // three-piece split of two floats (exact residuals: x - bf16(x) is representable in f32)
 __device__ __forceinline__ void split2(float a, float b, bf16x2& p0, bf16x2& p1, bf16x2& p2) {
   const f32x2 x = {a, b};
@@ -253,6 +245,13 @@ __device__ __forceinline__ bf16x8 rd16(const char* L, int off) { return *reinter
 __device__ __forceinline__ s16x4 rdtr(const char* L, int off) {
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(L + off));
+}
+
+// x(lane) + x(lane ^ 32) in every lane, in the order lower half + upper half (v_permlane32_swap:
+// lanes 0-31 of the first result take lanes 32-63 of the source, lanes 32-63 of the second take 0-31)
+__device__ __forceinline__ float xhalf_sum(float x) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(p[1]) + __uint_as_float(p[0]);
 }
 
 __device__ __forceinline__ bf16x8 cat_tr(s16x4 lo, s16x4 hi) {
@@ -387,7 +386,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   __syncthreads();
 
 #if defined(QD_LPROBE)
-  uint64_t stp[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t stp[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   for (int rd = 0; rd < rounds; rd++) {
     const int base = s0 + rd * RND;
@@ -457,8 +456,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_H1P + p * IMG + off) = x.p[p];
       }
     }
-    X3_BAR();  // B2: H1 image complete
     LP(2);
+    X3_BAR();  // B2: H1 image complete
+    LP(3);
 
 #if !defined(QD_X3_NOL2)
     // ---- L2 (E form): h2^T block w, A = W2 rows (pre-split pieces), B = H1 row reads
@@ -504,42 +504,41 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     // here it has the rest of the round (the dh1 pieces are waited ~10k cycles later)
     gather(next_row);
     next_row = index_of(rd + 2);
-    LP(3);
+    LP(4);
     if constexpr (DUMP) {
       LP_DUMP(for (int t = 0; t < 2; t++)
         if (valid[t])
           for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 1, 32 * w + acc_row(r, h), h2[t][r]));
     }
-    // head partial sums over the wave's 32 neurons (the two lane halves hold 16 each)
+    // head partial sums over the wave's 32 neurons (the two lane halves hold 16 each): the 2 x NOUT
+    // chains (each in neuron order) interleaved, so a dependent FMA waits on no other; the halves'
+    // sum by v_permlane32_swap (a VALU swap; the shuffle was an LDS round trip per output)
+    {
+      float part[2][NOUT];
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
-      float part[NOUT];
+      for (int t = 0; t < 2; t++)
 #pragma unroll
-      for (int k = 0; k < NOUT; k++) part[k] = 0.f;
+        for (int k = 0; k < NOUT; k++) part[t][k] = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; r++) {
-        h2[t][r] = relu(h2[t][r]);
         const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * (32 * w + acc_row(r, h)));
         const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
-        if constexpr (NOUT == ACT && QD_X3_PK) {  // two v_pk_fma_f32: the same four fmas
-          const f32x2 hh = {h2[t][r], h2[t][r]};
-          f32x2 p01 = {part[0], part[1]}, p23 = {part[2], part[3]};
-          p01 = __builtin_elementwise_fma(f32x2{wk[0], wk[1]}, hh, p01);
-          p23 = __builtin_elementwise_fma(f32x2{wk[2], wk[3]}, hh, p23);
-          part[0] = p01[0]; part[1] = p01[1]; part[2] = p23[0]; part[3] = p23[1];
-        } else {
 #pragma unroll
-          for (int k = 0; k < NOUT; k++) part[k] = fmaf(wk[k], h2[t][r], part[k]);
-        }
-      }
+        for (int t = 0; t < 2; t++) h2[t][r] = relu(h2[t][r]);
 #pragma unroll
-      for (int k = 0; k < NOUT; k++) {
-        const float o = __shfl_xor(part[k], 32);
-        if (h == 0) Lf[B_PART / 4 + (w * RND + 32 * t + l32) * 4 + k] = part[k] + o;
+        for (int k = 0; k < NOUT; k++)
+#pragma unroll
+          for (int t = 0; t < 2; t++) part[t][k] = fmaf(wk[k], h2[t][r], part[t][k]);
       }
+      // both halves hold the same sum (lo + hi == hi + lo) and write it to the same word
+#pragma unroll
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int k = 0; k < NOUT; k++) Lf[B_PART / 4 + (w * RND + 32 * t + l32) * 4 + k] = xhalf_sum(part[t][k]);
     }
+    LP(5);
     X3_BAR();  // B3: head partials complete
-    LP(4);
+    LP(6);
 
     // ---- per-row loss terms and dL/d(head output) (every wave, identical arithmetic)
     float d[2][NOUT];
@@ -571,23 +570,21 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         const float dlp = valid[t] ? -g.inv_batch * A * (w1 + (1.f - w1) * inr) * r : 0.f;
 #pragma unroll
         for (int k = 0; k < ACT; k++) d[t][k] = dlp * z[k] * isd[k];
-        if (acc_lane && valid[t]) {
-          st[0] += -fminf(sa, sb);
-          st[2] += fabsf(r - 1.f) > g.clip ? 1.f : 0.f;
+        // the row sums as selects, not branches (the same operations on the accumulating lanes)
+        const bool acc = acc_lane && valid[t];
+        st[0] = acc ? st[0] + -fminf(sa, sb) : st[0];
+        st[2] = acc ? st[2] + (fabsf(r - 1.f) > g.clip ? 1.f : 0.f) : st[2];
 #pragma unroll
-          for (int k = 0; k < ACT; k++) dls[k] += dlp * (z[k] * z[k] - 1.f);
-        }
+        for (int k = 0; k < ACT; k++) dls[k] = acc ? dls[k] + dlp * (z[k] * z[k] - 1.f) : dls[k];
       } else {
         const float diff = out[0] - SCI[e * 8 + 6];
         d[t][0] = valid[t] ? 2.f * g.vf_coef * g.inv_batch * diff : 0.f;
-        if (acc_lane && valid[t]) st[1] += diff * diff;
+        st[1] = acc_lane && valid[t] ? st[1] + diff * diff : st[1];
       }
-      if (acc_lane) {
 #pragma unroll
-        for (int k = 0; k < NOUT; k++) db3[k] += d[t][k];
-      }
+      for (int k = 0; k < NOUT; k++) db3[k] = acc_lane ? db3[k] + d[t][k] : db3[k];
     }
-    LP(5);
+    LP(7);
     // ---- dh2 (E form) -> DH2 pieces; dW3 per lane
 #pragma unroll
     for (int t = 0; t < 2; t++) {
@@ -603,16 +600,8 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
           for (int k = 0; k < NOUT; k++) gsum = fmaf(wk[k], d[t][k], gsum);
           v[u] = h2[t][r] > 0.f ? gsum : 0.f;
-          if constexpr (NOUT == ACT && QD_X3_PK) {  // two v_pk_fma_f32: the same four fmas
-            const f32x2 hh = {h2[t][r], h2[t][r]};
-            f32x2 a01 = {dW3[0][r], dW3[1][r]}, a23 = {dW3[2][r], dW3[3][r]};
-            a01 = __builtin_elementwise_fma(f32x2{d[t][0], d[t][1]}, hh, a01);
-            a23 = __builtin_elementwise_fma(f32x2{d[t][2], d[t][3]}, hh, a23);
-            dW3[0][r] = a01[0]; dW3[1][r] = a01[1]; dW3[2][r] = a23[0]; dW3[3][r] = a23[1];
-          } else {
 #pragma unroll
-            for (int k = 0; k < NOUT; k++) dW3[k][r] = fmaf(d[t][k], h2[t][r], dW3[k][r]);  // h2: relu'd
-          }
+          for (int k = 0; k < NOUT; k++) dW3[k][r] = fmaf(d[t][k], h2[t][r], dW3[k][r]);  // h2: relu'd
           dB2[r] += v[u];
         }
         const X3h x = split4(v);
@@ -621,9 +610,10 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_DH2P + p * IMG + off) = x.p[p];
       }
     }
+    LP(8);
     X3_BAR();  // B4: DH2 image complete
     const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);  // dh1's first two k-steps: in flight through dW2
-    LP(6);
+    LP(9);
 
 #if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
@@ -660,8 +650,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
 #endif
-    LP(7);
-    LP(8);
+    LP(10);
 #if !defined(QD_X3_NODH1)
     // ---- dh1 (R form) = relu'(h1) . (dh2 W2[:, block w]); then the dW1 slab (+ db1 in column 12)
     f32x16 dh1[2];
@@ -700,7 +689,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     }
 #pragma unroll
     for (int t = 0; t < 2; t++) dh1[t] += dh1s[t];
-    LP(9);
+    LP(11);
     // this round's dW1 in fresh accumulators (big / small terms), added to the launch total with
     // round-to-nearest VALU adds: one MFMA chain over every row of the block drifted by the
     // truncation bias (mma3s). The previous round's are added here, a round after their MFMAs
@@ -741,13 +730,13 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
   #endif
-    LP(10);
+    LP(12);
 }
   dW1 += dW1b + dW1s;
 #if defined(QD_LPROBE)
   if (DUMP && lane == 0) {
     uint64_t* o = reinterpret_cast<uint64_t*>(g.dump) + (size_t(blockIdx.x) * 8 + (NOUT == ACT ? 0 : 4) + size_t(w)) * 16;
-    for (int k = 0; k < 11; k++) o[k] = stp[k];
+    for (int k = 0; k < 13; k++) o[k] = stp[k];
     o[15] = NOUT;
   }
 #endif
