@@ -58,3 +58,21 @@ def test_world_size_mismatch_is_refused():
                        capture_output=True, text=True, timeout=60)
     assert r.returncode != 0
     assert "--gpus 1" in r.stderr
+
+
+def test_launch_terms_arithmetic():
+    """roofline.frac_beyond_launch_floor / frac_ceiling_one_launch (bench.py _launch_terms): the
+    HBM fraction of the time past the dispatch floor, and what a zero-latency one-launch step of the
+    same bytes could reach -- 18.2 MB at 8 TB/s = 2.28 us beside a 1.62 us floor caps it at 0.58."""
+    sys.path.insert(0, REPO)
+    import bench
+    byt = bench.BYTES_PER_ENV_STEP * 65536
+    at_peak_us = byt / (bench.HBM_PEAK_GBS * 1e3)
+    d = bench._launch_terms({"launch_floor_us": 1.62, "kernel_us": 5.94}, 65536)
+    assert d["launch_floor_us"] == 1.62
+    assert abs(d["frac_ceiling_one_launch"] - at_peak_us / (at_peak_us + 1.62)) < 1e-12
+    assert 0.58 < d["frac_ceiling_one_launch"] < 0.59
+    assert abs(d["frac_beyond_launch_floor"] - at_peak_us / (5.94 - 1.62)) < 1e-12
+    # no floor measured (or a kernel faster than it): no derived fields, never a division by <= 0
+    assert bench._launch_terms({"kernel_us": 5.94}, 65536) == {}
+    assert bench._launch_terms({"launch_floor_us": 2.0, "kernel_us": 1.5}, 65536)["frac_beyond_launch_floor"] is None
