@@ -42,25 +42,32 @@ struct KParams {
 // for the load burst and held until the matching store: ~54 VGPRs and 2 waves per SIMD.) Other
 // per-env arrays use the global saddr form: uniform base + 32-bit byte offset.
 __device__ __forceinline__ uint32_t env_off(uint32_t i) { return (i >> 6) * TILE_BYTES + (i & 63u) * 4u; }
+// cache-policy bits of the state loads / stores (A/B builds: 2 = nt)
+#ifndef QD_TILES_LD_AUX
+#define QD_TILES_LD_AUX 0
+#endif
+#ifndef QD_TILES_ST_AUX
+#define QD_TILES_ST_AUX 0
+#endif
 struct Tiles {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ explicit Tiles(const KParams& p)
       : r(__builtin_amdgcn_make_buffer_rsrc(p.tiles, 0, int(p.tile_bytes), 0x00020000)) {}
   // f must fold to a constant (unrolled loops): a lane-varying f would make the SGPR part divergent
   __device__ __forceinline__ uint32_t ldu(int f, uint32_t vo) const {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, 0);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, QD_TILES_LD_AUX);
   }
   __device__ __forceinline__ void stu(int f, uint32_t vo, uint32_t x) const {
-    __builtin_amdgcn_raw_buffer_store_b32(x, r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(x, r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, QD_TILES_ST_AUX);
   }
   __device__ __forceinline__ float ld(int f, uint32_t vo) const { return __builtin_bit_cast(float, ldu(f, vo)); }
   __device__ __forceinline__ void st(int f, uint32_t vo, float x) const { stu(f, vo, __builtin_bit_cast(uint32_t, x)); }
   // lane-varying field (k_step_g with G > 1): the whole offset in the VGPR
   __device__ __forceinline__ float ldv(int f, uint32_t vo) const {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f) * 256u, 0, 0));
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f) * 256u, 0, QD_TILES_LD_AUX));
   }
   __device__ __forceinline__ void stv(int f, uint32_t vo, float x) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), r, vo + uint32_t(f) * 256u, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), r, vo + uint32_t(f) * 256u, 0, QD_TILES_ST_AUX);
   }
 };
 template <typename T>
