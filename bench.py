@@ -122,21 +122,22 @@ def _kernel_name(env) -> str:
     form = int(N.lib().quad_kernel_form(env._h))
     lanes = form & 15
     name = (f"k_step_g<{lanes}>" if lanes else ("k_step_h" if form & 32 else "k_step")) + "<HOVER,noCTBR>"
-    tags = (["SPEC constants"] if form & 16 else []) + (["helper waves draw the resets"] if form & 32 else [])
+    tags = (["SPEC constants"] if form & 16 else []) + (["helper waves draw the resets"] if form & 32 else []) + \
+        (["nt state loads/stores"] if form & 256 else [])
     return name + (f" ({', '.join(tags)})" if tags else "")
 
 
 def _kernel_symbol(env) -> str:
     """The launched hover step kernel's template symbol as rocprofv3 names it (csrc/quadenv.hip
-    quad_step_range: k_step_h<KIND, CTBR, SPEC, HB> with HB from quad_kernel_form bit 7 (256-env
-    blocks above 32,768 envs, else 64); k_step<KIND, CTBR, SPEC>; k_step_g<KIND, CTBR, G, SPEC>)."""
+    quad_step_range: k_step_h<KIND, CTBR, SPEC, HB, NT> with HB from quad_kernel_form bit 7 (256-env
+    blocks above 32,768 envs, else 64) and NT (the state's nt cache policy) from bit 8; k_step<KIND, CTBR, SPEC>; k_step_g<KIND, CTBR, G, SPEC>)."""
     from uav_reinforcement_learning_control_amd import _native as N
     form = int(N.lib().quad_kernel_form(env._h))
     lanes, spec = form & 15, "true" if form & 16 else "false"
     if lanes:
         return f"k_step_g<0, false, {lanes}, {spec}>"
     if form & 32:
-        return f"k_step_h<0, false, {spec}, {256 if form & 128 else 64}>"
+        return f"k_step_h<0, false, {spec}, {256 if form & 128 else 64}, {'true' if form & 256 else 'false'}>"
     return f"k_step<0, false, {spec}>"
 
 

@@ -49,6 +49,7 @@ def spec_mode(request, monkeypatch):
     monkeypatch.setenv("QUADENV_LANES", "0")
     monkeypatch.setenv("QUADENV_HELPER", "1")
     monkeypatch.delenv("QUADENV_HBLOCK", raising=False)
+    monkeypatch.delenv("QUADENV_NT", raising=False)
     return request.param
 
 
@@ -130,7 +131,8 @@ def _operand_slack(g, ref, st, rows):
 def test_full_batch_step_matches_oracle(golden_dir, env_name, wrapper, kind, wrap, fixture, spec_mode):
     st, acts, d, ng = _batch(golden_dir, fixture, kind, wrap)
     env, form = _env(env_name, wrapper, auto_reset=False)
-    assert form == (32 | 128 | (16 if spec_mode == "1" else 0)), form  # k_step_h, 256-env blocks
+    # k_step_h, 256-env blocks, nt state policy: the headline's instantiation
+    assert form == (32 | 128 | 256 | (16 if spec_mode == "1" else 0)), form
     env.set_state(**st)
     obs, rew, te, tr, inf = env.step(torch.from_numpy(acts).cuda(), info="full")
     torch.cuda.synchronize()

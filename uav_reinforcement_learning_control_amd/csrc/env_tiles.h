@@ -42,34 +42,36 @@ struct KParams {
 // for the load burst and held until the matching store: ~54 VGPRs and 2 waves per SIMD.) Other
 // per-env arrays use the global saddr form: uniform base + 32-bit byte offset.
 __device__ __forceinline__ uint32_t env_off(uint32_t i) { return (i >> 6) * TILE_BYTES + (i & 63u) * 4u; }
-// cache-policy bits of the state loads / stores (A/B builds: 2 = nt)
-#ifndef QD_TILES_LD_AUX
-#define QD_TILES_LD_AUX 0
-#endif
-#ifndef QD_TILES_ST_AUX
-#define QD_TILES_ST_AUX 0
-#endif
-struct Tiles {
+// Cache policy of the state loads and stores (AUX: 0 = default, 2 = nt): a template parameter of
+// the step kernel, chosen by batch size at launch (quad_step_range). A step reads and writes each
+// env's fields once; at the DRAM-bound sizes nt keeps them out of L2 and the Infinity Cache (2M envs
+// 97 vs 149 us, 4M 268 vs 317, 8M 546 vs 634 for k_step_h), at 65,536 envs it spares the
+// end-of-launch write-back of the dirty state lines (5.60-5.81 vs 5.83-5.92 us), and from 4,096 to
+// 1M envs, where the next step reads the state back from the Infinity Cache, it costs 0-17 %
+// (profiles/r04/r4_step_forms_nt.txt, r4_step_nt_sizes.txt). nt loads alone were slower.
+template <int AUX>
+struct TilesA {
   __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ explicit Tiles(const KParams& p)
+  __device__ __forceinline__ explicit TilesA(const KParams& p)
       : r(__builtin_amdgcn_make_buffer_rsrc(p.tiles, 0, int(p.tile_bytes), 0x00020000)) {}
   // f must fold to a constant (unrolled loops): a lane-varying f would make the SGPR part divergent
   __device__ __forceinline__ uint32_t ldu(int f, uint32_t vo) const {
-    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, QD_TILES_LD_AUX);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, AUX);
   }
   __device__ __forceinline__ void stu(int f, uint32_t vo, uint32_t x) const {
-    __builtin_amdgcn_raw_buffer_store_b32(x, r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, QD_TILES_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(x, r, vo + uint32_t(f & 15) * 256u, uint32_t(f >> 4) * 4096u, AUX);
   }
   __device__ __forceinline__ float ld(int f, uint32_t vo) const { return __builtin_bit_cast(float, ldu(f, vo)); }
   __device__ __forceinline__ void st(int f, uint32_t vo, float x) const { stu(f, vo, __builtin_bit_cast(uint32_t, x)); }
   // lane-varying field (k_step_g with G > 1): the whole offset in the VGPR
   __device__ __forceinline__ float ldv(int f, uint32_t vo) const {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f) * 256u, 0, QD_TILES_LD_AUX));
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f) * 256u, 0, AUX));
   }
   __device__ __forceinline__ void stv(int f, uint32_t vo, float x) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), r, vo + uint32_t(f) * 256u, 0, QD_TILES_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), r, vo + uint32_t(f) * 256u, 0, AUX);
   }
 };
+using Tiles = TilesA<0>;
 template <typename T>
 __device__ __forceinline__ T ldo(const T* b, uint32_t off) {
   return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(b) + off);
@@ -79,8 +81,9 @@ __device__ __forceinline__ void sto(T* b, uint32_t off, T v) {
   *reinterpret_cast<T*>(reinterpret_cast<char*>(b) + off) = v;
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void load_env(const KParams& p, int i, EnvRegs<float>& e, bool ctbr) {
-  const Tiles S(p);
+  const TilesA<AUX> S(p);
   const uint32_t o = env_off(uint32_t(i));
 #pragma unroll
   for (int j = 0; j < 3; j++) e.pos[j] = S.ld(F_QPOS + j, o);
@@ -108,8 +111,9 @@ __device__ __forceinline__ void load_env(const KParams& p, int i, EnvRegs<float>
 
 // the fields the physics and the observation need (not the voltage / CTBR integral: k_step_h's
 // helper waves own the control path)
+template <int AUX = 0>
 __device__ __forceinline__ void load_env_motion(const KParams& p, int i, EnvRegs<float>& e) {
-  const Tiles S(p);
+  const TilesA<AUX> S(p);
   const uint32_t o = env_off(uint32_t(i));
 #pragma unroll
   for (int j = 0; j < 3; j++) e.pos[j] = S.ld(F_QPOS + j, o);
@@ -128,9 +132,10 @@ __device__ __forceinline__ void load_env_motion(const KParams& p, int i, EnvRegs
   e.step = int32_t(S.ldu(F_STEP, o));
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void store_env(const KParams& p, int i, const EnvRegs<float>& e,
                                           bool ctbr) {
-  const Tiles S(p);
+  const TilesA<AUX> S(p);
   const uint32_t o = env_off(uint32_t(i));
 #pragma unroll
   for (int j = 0; j < 3; j++) S.st(F_QPOS + j, o, e.pos[j]);

@@ -301,16 +301,17 @@ constexpr int H_SMALL = 32768;
 #endif
 constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
 constexpr int HCTL = 9;   // floats per env from the control helper: Fsum, taum 3, volt, bad ctrl, rint 3
-template <int KIND, bool CTBR, int HB>
+template <int KIND, bool CTBR, int HB, bool NT>
 __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, const float4* __restrict__ act,
                                             QuadStepOut out, float4* lds, float* H, float* CT) {
+  constexpr int AUX = NT ? 2 : 0;  // the state tiles' cache policy (env_tiles.h)
   const int tid = threadIdx.x;
   const int block_first = p.first + blockIdx.x * HB;
   const int end = p.first + p.count;
   const int l = tid & (HB - 1);
   const bool live = block_first + l < end;
   const int i = live ? block_first + l : end - 1;
-  const Tiles S(p);
+  const TilesA<AUX> S(p);
   const uint32_t vo = env_off(uint32_t(i));
 #if defined(QD_PROBE)  // tools/probe/probe_step_h.py: per-wave stamps into the target_info buffer
   uint64_t stamp_buf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -401,7 +402,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     float obs[12];
     EnvRegs<float> e;
 #if defined(QD_H_NOCTL)  // A/B builds only: the step wave runs the control path itself (round 2)
-    load_env(p, i, e, CTBR);
+    load_env<AUX>(p, i, e, CTBR);
     const uint32_t ep = S.ldu(F_EP, vo);
     const float4 a4 = act[i];
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
@@ -409,7 +410,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     env_step<float, CTBR>(K, e, a, r);
     __syncthreads();  // (C)
 #else
-    load_env_motion(p, i, e);
+    load_env_motion<AUX>(p, i, e);
     const uint32_t ep = S.ldu(F_EP, vo);
     if (stamps) { QD_PIN(ep); QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.th, 4); QD_PIN_N(e.v, 3);
                   QD_PIN_N(e.w, 3); QD_PIN_N(e.s, 4); QD_PIN_N(e.target, 3); QD_PIN(e.step); }
@@ -484,7 +485,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
       e.step = 0;
       S.stu(F_EP, vo, ep + 1u);
     }
-    if (live) store_env(p, i, e, CTBR);
+    if (live) store_env<AUX>(p, i, e, CTBR);
     lds[3 * l + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
     lds[3 * l + 1] = make_float4(obs[4], obs[5], obs[6], obs[7]);
     lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
@@ -510,7 +511,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #endif
 }
 
-template <int KIND, bool CTBR, bool SPEC, int HB>
+template <int KIND, bool CTBR, bool SPEC, int HB, bool NT>
 __global__ __launch_bounds__(2 * HB) void k_step_h(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
                                                       int32_t first, int32_t count,
                                                       const KConsts<float>* __restrict__ kc, KParams p, QuadStepOut out) {
@@ -521,9 +522,9 @@ __global__ __launch_bounds__(2 * HB) void k_step_h(float* tiles, const float4* _
   __shared__ float CT[(CTBR ? HCTL : HCTL - 3) * HB];
   if constexpr (SPEC) {
     constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
-    step_h_body<KIND, CTBR, HB>(K, p, act, out, lds, H, CT);
+    step_h_body<KIND, CTBR, HB, NT>(K, p, act, out, lds, H, CT);
   } else {
-    step_h_body<KIND, CTBR, HB>(*kc, p, act, out, lds, H, CT);
+    step_h_body<KIND, CTBR, HB, NT>(*kc, p, act, out, lds, H, CT);
   }
 }
 
@@ -1583,6 +1584,7 @@ struct QuadHandle {
   bool spec = false;                 // kh == a reference default block: k_step's SPEC form
   bool helper = true;                // one-thread form: k_step_h (helper waves draw the resets)
   int hblock = 0;                    // envs per k_step_h block: 0 = by size (64 up to H_SMALL, else 256)
+  int nt = -1;                       // k_step_h's state cache policy: -1 = by size (nt_state), 0 / 1
 };
 
 namespace {
@@ -1599,6 +1601,15 @@ struct DeviceGuard {
     if (prev >= 0) (void)hipSetDevice(prev);
   }
 };
+
+// k_step_h's state cache policy for a launch of `count` envs (env_tiles.h): nt where it measured
+// faster -- one step wave per SIMD (65,536 envs) and the DRAM-bound sizes from 2M envs -- and the
+// default policy where the next step reads the state back from the Infinity Cache (4,096 and
+// 262,144 .. 1M envs; 32,768 measured equal). QUADENV_NT=0 / 1 pins it (A/B and tests).
+bool nt_state(const QuadHandle* h, int64_t count) {
+  if (h->nt >= 0) return h->nt != 0;
+  return (count > H_SMALL && count < (int64_t(1) << 17)) || count >= (int64_t(1) << 21);
+}
 
 }  // namespace
 
@@ -1654,6 +1665,7 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   // QUADENV_HELPER=0 keeps the plain k_step (A/B and tests)
   if (const char* v = std::getenv("QUADENV_HELPER")) h->helper = std::atoi(v) != 0;
   // QUADENV_HBLOCK=64|256 pins the helper form's block size (tests run the 256-env blocks at small N)
+  if (const char* v = std::getenv("QUADENV_NT")) h->nt = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("QUADENV_HBLOCK")) {
     const int b = std::atoi(v);
     if (b == 64 || b == 256) h->hblock = b;
@@ -1680,12 +1692,12 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   h->kp.auto_reset = cfg->auto_reset;
   h->kp.seed = seed;
   h->kp.gid_base = env_id_base;
-  // measured on MI355X (DESIGN.md "Step-kernel forms"): the one-thread k_step is fastest while
-  // the batch is about one wave per SIMD; the k_step_g<1> form wins once waves queue up, up to the
-  // batches whose state the 256 MB Infinity Cache holds; past them (true HBM) two lanes per env
-  // (k_step_g<2>: more waves in flight per SIMD) win -- 2M envs 141 vs 152 us, 4M 303 vs 326, 8M
-  // 610 vs 639 (round 4, tools/dram_sweep.py; 1M: 52.8 vs 62.5 the other way)
-  h->lanes = n_envs < (1 << 18) ? 0 : (n_envs <= (1 << 20) ? 1 : 2);
+  // measured on MI355X (round 4, tools/step_env_ab.py, profiles/r04/r4_step_forms_nt.txt and
+  // r4_step_nt_sizes.txt): the helper-wave form k_step_h (256-env blocks above 32,768 envs) with
+  // its size-chosen cache policy (nt_state) is the fastest form at every size -- 262,144 envs 14.4
+  // vs 15.9 us for k_step_g<1>, 1M 51.1 vs 51.9, 2M 97 vs 117 for k_step_g<2> (both nt), 4M 268.6 vs
+  // 268.3, 8M 546 vs 557; the lane-group forms k_step_g<G> stay selectable (QUADENV_LANES)
+  h->lanes = 0;
   if (const char* v = std::getenv("QUADENV_LANES")) {
     const int g = std::atoi(v);
     if (g == 0 || g == 1 || g == 2 || g == 4) h->lanes = g;
@@ -1712,7 +1724,7 @@ int32_t quad_kernel_form(const QuadHandle* h) {
   if (wrap_relpos(h->cfg.wrapper) || h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) return 64;
   const bool wide = h->hblock ? h->hblock == 256 : h->n > H_SMALL;
   return h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0) |
-         (h->lanes == 0 && h->helper && wide ? 128 : 0);
+         (h->lanes == 0 && h->helper && wide ? 128 : 0) | (h->lanes == 0 && h->helper && nt_state(h, h->n) ? 256 : 0);
 }
 
 int quad_seed(QuadHandle* h, uint64_t seed, void* stream) {
@@ -1799,16 +1811,19 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, QD_KARGS);     \
   else                                                                                          \
     hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, QD_KARGS);
-#define QD_LAUNCH_H(SP, HB)                                                                            \
+#define QD_LAUNCH_H2(SP, HB, NT)                                                                       \
   if (traj && ctbr)                                                                             \
-    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, true, SP, HB>), grid, blk2, 0, s, QD_KARGS);      \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, true, SP, HB, NT>), grid, blk2, 0, s, QD_KARGS);      \
   else if (traj)                                                                                \
-    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, false, SP, HB>), grid, blk2, 0, s, QD_KARGS);     \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, false, SP, HB, NT>), grid, blk2, 0, s, QD_KARGS);     \
   else if (ctbr)                                                                                \
-    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, true, SP, HB>), grid, blk2, 0, s, QD_KARGS);     \
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, true, SP, HB, NT>), grid, blk2, 0, s, QD_KARGS);     \
   else                                                                                          \
-    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, false, SP, HB>), grid, blk2, 0, s, QD_KARGS);
+    hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, false, SP, HB, NT>), grid, blk2, 0, s, QD_KARGS);
+#define QD_LAUNCH_H(SP, HB) \
+  if (nt) { QD_LAUNCH_H2(SP, HB, true) } else { QD_LAUNCH_H2(SP, HB, false) }
     const bool wide = h->hblock ? h->hblock == 256 : count > H_SMALL;
+    const bool nt = nt_state(h, count);
     if (h->helper && !wide) {
       const dim3 grid(unsigned((int64_t(count) + 63) / 64)), blk2(128);
       if (h->spec) { QD_LAUNCH_H(true, 64) } else { QD_LAUNCH_H(false, 64) }
@@ -1818,6 +1833,7 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     } else if (h->spec) { QD_LAUNCH_K(true) } else { QD_LAUNCH_K(false) }
 #undef QD_LAUNCH_K
 #undef QD_LAUNCH_H
+#undef QD_LAUNCH_H2
 #undef QD_KARGS
   } else {
     const dim3 grid(unsigned((int64_t(count) * G + BLOCK - 1) / BLOCK));
