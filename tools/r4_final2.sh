@@ -20,5 +20,4 @@ step r4g_bench 400 python -u bench.py --gpus 1 --steps 20 --warmup 5
 step r4g_rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4g_prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
 step r4g_issue 500 env SIZES="65536 1048576 4194304" bash tools/pmc/issue_roofline.sh
 step r4g_traffic 500 bash tools/pmc/traffic_round.sh
-step r4g_sizes 700 bash tools/r4_nt_sizes.sh
 echo "=== done"
