@@ -356,7 +356,15 @@ def _dp_worker(rank, world, port, q):
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)  # both ranks share cuda:0 here
         from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+        from uav_reinforcement_learning_control_amd.ppo import ppo as PP
         from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
+        perms, draw = [], PP.epoch_permutation
+
+        def recorded(total, device):  # the minibatch order this rank's update used
+            p = draw(total, device)
+            perms.append(p.cpu().numpy())
+            return p
+        PP.epoch_permutation = recorded
         n = DP_ENVS
         env = QuadVecEnv(n, env="hover", device="cuda:0", seed=5, env_id_base=rank * n)
         algo = PPO(env, PPOConfig(n_steps=DP_STEPS, n_minibatches=4, n_epochs=1), seed=3)
@@ -366,6 +374,7 @@ def _dp_worker(rank, world, port, q):
         bufs = {k: getattr(algo, k).cpu().numpy() for k in DP_BUFFERS}
         st = algo.train()
         p1 = torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()]).cpu()
+        bufs["perms"] = perms
         q.put((rank, p0.numpy(), p1.numpy(), st["n"], bufs))
         env.close()
         dist.destroy_process_group()
@@ -375,7 +384,8 @@ def _dp_worker(rank, world, port, q):
 
 def test_fused_update_two_ranks_stay_in_sync():
     """Data-parallel PPO with the fused update: 2 ranks (gloo, one GPU), different env shards,
-    one all-reduce per optimizer step -> identical parameters on both ranks after the update."""
+    one all-reduce per optimizer step -> identical parameters on both ranks after the update, equal
+    bit for bit to one process replaying both shards' minibatches with the averaged gradient."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
@@ -411,6 +421,39 @@ def test_fused_update_two_ranks_stay_in_sync():
         if k == "buf_start":
             resets = int(full[1:].sum())
     assert resets > 0  # the window covers auto-resets
+    env.close()
+    # ... and the update is the mean of the shards' minibatch gradients: one process replays both
+    # ranks' minibatches (their buffers, their recorded permutations) through the same learner,
+    # averages the two gradients as the all-reduce does (SUM, then / world) and takes the same
+    # clip + Adam step -- the parameters after the 4 optimizer steps are the ranks' bit for bit
+    env = QuadVecEnv(DP_ENVS, env="hover", device="cuda:0", seed=5)
+    emu = PPO(env, PPOConfig(n_steps=DP_STEPS, n_minibatches=4, n_epochs=1), seed=3)
+    assert emu.world == 1 and emu._learner is not None
+    dev = torch.device("cuda:0")
+    shard = []
+    for r in range(2):
+        b = res[r][3]
+        assert len(b["perms"]) == 1
+        total = DP_STEPS * DP_ENVS
+        shard.append(dict(obs=torch.from_numpy(b["buf_obs"]).to(dev).reshape(total, 12),
+                          act=torch.from_numpy(b["buf_act"]).to(dev).reshape(total, 4),
+                          logp=torch.from_numpy(b["buf_logp"]).to(dev).reshape(total),
+                          adv=torch.from_numpy(b["buf_adv"]).to(dev).reshape(total),
+                          ret=torch.from_numpy(b["buf_ret"]).to(dev).reshape(total),
+                          perm=torch.from_numpy(b["perms"][0]).to(dev)))
+    assert not torch.equal(shard[0]["perm"], shard[1]["perm"])  # each rank draws its own order
+    B = emu.batch
+    for m in range(4):
+        g = []
+        for s in shard:
+            idx = s["perm"][m * B:(m + 1) * B].contiguous()
+            emu._learner.grads(s["obs"], s["act"], s["logp"], s["adv"], s["ret"], idx)
+            g.append(emu._flat.clone())
+        emu._flat.copy_(g[0] + g[1]).div_(2)
+        emu._adam.step()
+    torch.cuda.synchronize()
+    pe = torch.cat([p.detach().reshape(-1) for p in emu.policy.parameters()]).cpu().numpy()
+    np.testing.assert_array_equal(pe, b0)
     env.close()
 
 
