@@ -151,8 +151,8 @@ int32_t quad_num_envs(const QuadHandle* h);
  * per env; 1/2/4 = k_step_g), bit 4 set when the handle's constant block is a reference default and
  * the kernels with compiled-in constants run (QUADENV_SPEC=0 turns that off), bit 5 set when the
  * one-thread form runs with helper waves drawing the resets (k_step_h; QUADENV_HELPER=0 turns it off),
- * bit 7 set when those helper blocks are 256 envs wide (full-batch steps above 32,768 envs, or
- * QUADENV_HBLOCK=256; 64-env blocks otherwise), bit 8 set when a full-batch step of those blocks
+ * bit 7 set when those helper blocks are 256 envs wide (full-batch steps of 32,769 .. 2,097,151 envs,
+ * or QUADENV_HBLOCK=256; 64-env blocks otherwise), bit 8 set when a full-batch step of those blocks
  * moves the env state with the nt cache policy (65,536-env-scale and >= 2M-env batches; QUADENV_NT
  * pins it). 64 alone: a RELPOS or brax handle, whose one step kernel (k_step_relpos / k_step_brax) has no forms. */
 int32_t quad_kernel_form(const QuadHandle* h);

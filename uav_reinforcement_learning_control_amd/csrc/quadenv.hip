@@ -1583,7 +1583,7 @@ struct QuadHandle {
   KConsts<float>* kdev = nullptr;    // device copy the kernels read (scalar loads, K$-resident)
   bool spec = false;                 // kh == a reference default block: k_step's SPEC form
   bool helper = true;                // one-thread form: k_step_h (helper waves draw the resets)
-  int hblock = 0;                    // envs per k_step_h block: 0 = by size (64 up to H_SMALL, else 256)
+  int hblock = 0;                    // envs per k_step_h block: 0 = by size (h_wide: 256 between H_SMALL and 2M, else 64)
   int nt = -1;                       // k_step_h's state cache policy: -1 = by size (nt_state), 0 / 1
 };
 
@@ -1609,6 +1609,15 @@ struct DeviceGuard {
 bool nt_state(const QuadHandle* h, int64_t count) {
   if (h->nt >= 0) return h->nt != 0;
   return (count > H_SMALL && count < (int64_t(1) << 17)) || count >= (int64_t(1) << 21);
+}
+
+// k_step_h's block size for a launch of `count` envs: 256-env blocks above H_SMALL (the comment at
+// H_SMALL), back to 64 from 2M envs, where the state streams from DRAM with the nt policy: 4M
+// 264.2-264.5 vs 269.8-270.1 us, 2M 95.6-96.1 vs 97.7-98.4, 8M 545.7-546.9 vs 551.7-552.1, while 1M
+// keeps 256 (52.7 vs 55.5-55.8; profiles/r04/r4_step_hb_large.txt). QUADENV_HBLOCK pins it.
+bool h_wide(const QuadHandle* h, int64_t count) {
+  if (h->hblock) return h->hblock == 256;
+  return count > H_SMALL && count < (int64_t(1) << 21);
 }
 
 }  // namespace
@@ -1722,7 +1731,7 @@ int32_t quad_kernel_form(const QuadHandle* h) {
   // RELPOS and the brax kinds have one kernel each (k_step_relpos / k_step_brax): no lanes, SPEC
   // or helper forms to report
   if (wrap_relpos(h->cfg.wrapper) || h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) return 64;
-  const bool wide = h->hblock ? h->hblock == 256 : h->n > H_SMALL;
+  const bool wide = h_wide(h, h->n);
   return h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0) |
          (h->lanes == 0 && h->helper && wide ? 128 : 0) | (h->lanes == 0 && h->helper && nt_state(h, h->n) ? 256 : 0);
 }
@@ -1822,7 +1831,7 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, false, SP, HB, NT>), grid, blk2, 0, s, QD_KARGS);
 #define QD_LAUNCH_H(SP, HB) \
   if (nt) { QD_LAUNCH_H2(SP, HB, true) } else { QD_LAUNCH_H2(SP, HB, false) }
-    const bool wide = h->hblock ? h->hblock == 256 : count > H_SMALL;
+    const bool wide = h_wide(h, count);
     const bool nt = nt_state(h, count);
     if (h->helper && !wide) {
       const dim3 grid(unsigned((int64_t(count) + 63) / 64)), blk2(128);
