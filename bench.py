@@ -130,7 +130,7 @@ def _kernel_name(env) -> str:
 def _kernel_symbol(env) -> str:
     """The launched hover step kernel's template symbol as rocprofv3 names it (csrc/quadenv.hip
     quad_step_range: k_step_h<KIND, CTBR, SPEC, HB, NT> with HB from quad_kernel_form bit 7 (256-env
-    blocks above 32,768 envs, else 64) and NT (the state's nt cache policy) from bit 8; k_step<KIND, CTBR, SPEC>; k_step_g<KIND, CTBR, G, SPEC>)."""
+    blocks for 32,769 .. 2,097,151 envs, else 64) and NT (the state's nt cache policy) from bit 8; k_step<KIND, CTBR, SPEC>; k_step_g<KIND, CTBR, G, SPEC>)."""
     from uav_reinforcement_learning_control_amd import _native as N
     form = int(N.lib().quad_kernel_form(env._h))
     lanes, spec = form & 15, "true" if form & 16 else "false"
