@@ -123,7 +123,7 @@ def _kernel_name(env) -> str:
     lanes = form & 15
     name = (f"k_step_g<{lanes}>" if lanes else ("k_step_h" if form & 32 else "k_step")) + "<HOVER,noCTBR>"
     tags = (["SPEC constants"] if form & 16 else []) + (["helper waves draw the resets"] if form & 32 else []) + \
-        (["nt state loads/stores"] if form & 256 else [])
+        (["nt state loads/stores"] if form & 256 else []) + (["7-wave DRAM form k_step_hd"] if form & 512 else [])
     return name + (f" ({', '.join(tags)})" if tags else "")
 
 
@@ -136,6 +136,8 @@ def _kernel_symbol(env) -> str:
     lanes, spec = form & 15, "true" if form & 16 else "false"
     if lanes:
         return f"k_step_g<0, false, {lanes}, {spec}>"
+    if form & 512:
+        return f"k_step_hd<0, false, {spec}>"
     if form & 32:
         return f"k_step_h<0, false, {spec}, {256 if form & 128 else 64}, {'true' if form & 256 else 'false'}>"
     return f"k_step<0, false, {spec}>"

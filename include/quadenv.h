@@ -154,7 +154,8 @@ int32_t quad_num_envs(const QuadHandle* h);
  * bit 7 set when those helper blocks are 256 envs wide (full-batch steps of 32,769 .. 2,097,151 envs,
  * or QUADENV_HBLOCK=256; 64-env blocks otherwise), bit 8 set when a full-batch step of those blocks
  * moves the env state with the nt cache policy (65,536-env-scale and >= 2M-env batches; QUADENV_NT
- * pins it). 64 alone: a RELPOS or brax handle, whose one step kernel (k_step_relpos / k_step_brax) has no forms. */
+ * pins it), bit 9 set when those 64-env nt launches run as k_step_hd, the DRAM form with a
+ * 7-waves-per-SIMD register budget (>= 4M-env batches; QUADENV_HD pins it). 64 alone: a RELPOS or brax handle, whose one step kernel (k_step_relpos / k_step_brax) has no forms. */
 int32_t quad_kernel_form(const QuadHandle* h);
 
 /* Re-key the reset RNG (HoverEnv.reset(seed=...), hover_env.py:210 -> gymnasium seeding) and

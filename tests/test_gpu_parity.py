@@ -137,12 +137,13 @@ def _pre12(st, i):
     return np.concatenate([st["qpos"][i][:3], np.zeros(3, np.float32), st["qvel"][i][:6]])
 
 
-@pytest.fixture(params=["1", "2", "4", "0", "0t", "0w", "0wt", "0n"])
+@pytest.fixture(params=["1", "2", "4", "0", "0t", "0d", "0w", "0wt", "0n"])
 def kernel_variant(request, monkeypatch):
     """Every step kernel form must be exact: k_step_g with 1, 2 or 4 lanes per env, and the
     one-thread-per-env form (QUADENV_LANES=0) with helper waves drawing the resets (k_step_h, the
     default at every size) -- in 64-env blocks ("0", the form up to 32,768 envs; "0t" with the nt
-    state cache policy, forced by QUADENV_NT: the form from 2M envs) and in the 256-env blocks of
+    state cache policy, forced by QUADENV_NT: the form from 2M envs; "0d" the same as k_step_hd, the
+    7-waves-per-SIMD DRAM form of >= 4M-env batches, forced by QUADENV_HD) and in the 256-env blocks of
     the batches between ("0w", forced by QUADENV_HBLOCK; "0wt" with the nt policy of the
     65,536-env-scale batches) -- and without the helpers ("0n": k_step)."""
     monkeypatch.setenv("QUADENV_LANES", request.param[0])
@@ -151,10 +152,14 @@ def kernel_variant(request, monkeypatch):
         monkeypatch.setenv("QUADENV_HBLOCK", "256")
     else:
         monkeypatch.delenv("QUADENV_HBLOCK", raising=False)
-    if request.param.endswith("t"):
+    if request.param.endswith(("t", "d")):
         monkeypatch.setenv("QUADENV_NT", "1")
     else:
         monkeypatch.delenv("QUADENV_NT", raising=False)
+    if request.param.endswith("d"):
+        monkeypatch.setenv("QUADENV_HD", "1")
+    else:
+        monkeypatch.delenv("QUADENV_HD", raising=False)
     return request.param
 
 
@@ -169,10 +174,11 @@ def spec_mode(request, monkeypatch):
 def test_kernel_form_selection(spec_mode):
     from uav_reinforcement_learning_control_amd import _native as N
     # 32: helper waves (k_step_h, the form at every size), + 128: in 256-env blocks (32,769 ..
-    # 2,097,151 envs), + 256: with the nt state cache policy (65,536-env-scale batches and from 2M envs)
+    # 2,097,151 envs), + 256: with the nt state cache policy (65,536-env-scale batches and from 2M
+    # envs), + 512: as k_step_hd (from 4M envs)
     for n, form in ((4096, 32), (32768, 32), (32769, 32 | 128 | 256), (65536, 32 | 128 | 256),
                     (300000, 32 | 128), ((1 << 20) + 64, 32 | 128), ((1 << 21) - 64, 32 | 128),
-                    (1 << 21, 32 | 256)):
+                    (1 << 21, 32 | 256), ((1 << 22) - 64, 32 | 256), (1 << 22, 32 | 256 | 512)):
         e = _env(n)
         assert N.lib().quad_kernel_form(e._h) == form | (16 if spec_mode == "1" else 0), n
         e.close()

@@ -528,6 +528,29 @@ __global__ __launch_bounds__(2 * HB) void k_step_h(float* tiles, const float4* _
   }
 }
 
+// k_step_hd: k_step_h's DRAM form (64-env blocks, nt state) with a floor of 7 waves per SIMD on its
+// register budget (72 VGPRs, 5 of them spilled, instead of 75-76 and 6 waves). More waves keep more
+// state bytes in flight where the batch streams from DRAM: 4M envs 250.0-251.6 vs 264.9-265.8 us,
+// 8M 511.7-513.0 vs 546.5-547.9; where the Infinity Cache still serves part of it the spills cost
+// more than the waves buy (2M 108 vs 95, 3M 161 vs 145; profiles/r04/r4_step_hw7_ab.txt). Same body,
+// same bits.
+template <int KIND, bool CTBR, bool SPEC>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(7, 8)))
+void k_step_hd(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes, int32_t first, int32_t count,
+               const KConsts<float>* __restrict__ kc, KParams p, QuadStepOut out) {
+  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
+  p.kc = kc;
+  __shared__ float4 lds[64 * 3];
+  __shared__ float H[HROW * 64];
+  __shared__ float CT[(CTBR ? HCTL : HCTL - 3) * 64];
+  if constexpr (SPEC) {
+    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
+    step_h_body<KIND, CTBR, 64, true>(K, p, act, out, lds, H, CT);
+  } else {
+    step_h_body<KIND, CTBR, 64, true>(*kc, p, act, out, lds, H, CT);
+  }
+}
+
 // k_step: one env per thread. SPEC: the handle's constant block equals the reference default
 // (quad_create checks the bytes), so the constants are compiled in -- no scalar loads of the block
 // and no waits on them inside the step.
@@ -1584,6 +1607,7 @@ struct QuadHandle {
   bool spec = false;                 // kh == a reference default block: k_step's SPEC form
   bool helper = true;                // one-thread form: k_step_h (helper waves draw the resets)
   int hblock = 0;                    // envs per k_step_h block: 0 = by size (h_wide: 256 between H_SMALL and 2M, else 64)
+  int hd = -1;                       // k_step_hd for the 64-env nt launches: -1 = by size (hd_form), 0 / 1
   int nt = -1;                       // k_step_h's state cache policy: -1 = by size (nt_state), 0 / 1
 };
 
@@ -1618,6 +1642,13 @@ bool nt_state(const QuadHandle* h, int64_t count) {
 bool h_wide(const QuadHandle* h, int64_t count) {
   if (h->hblock) return h->hblock == 256;
   return count > H_SMALL && count < (int64_t(1) << 21);
+}
+
+// k_step_hd instead of k_step_h<.., 64, true> for a launch of `count` envs: from 4M envs, where the
+// step streams from DRAM (the comment at k_step_hd). QUADENV_HD=0 / 1 pins it (A/B and tests).
+bool hd_form(const QuadHandle* h, int64_t count) {
+  if (h_wide(h, count) || !nt_state(h, count)) return false;
+  return h->hd >= 0 ? h->hd != 0 : count >= (int64_t(1) << 22);
 }
 
 }  // namespace
@@ -1675,6 +1706,7 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   if (const char* v = std::getenv("QUADENV_HELPER")) h->helper = std::atoi(v) != 0;
   // QUADENV_HBLOCK=64|256 pins the helper form's block size (tests run the 256-env blocks at small N)
   if (const char* v = std::getenv("QUADENV_NT")) h->nt = std::atoi(v) != 0 ? 1 : 0;
+  if (const char* v = std::getenv("QUADENV_HD")) h->hd = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("QUADENV_HBLOCK")) {
     const int b = std::atoi(v);
     if (b == 64 || b == 256) h->hblock = b;
@@ -1733,7 +1765,8 @@ int32_t quad_kernel_form(const QuadHandle* h) {
   if (wrap_relpos(h->cfg.wrapper) || h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) return 64;
   const bool wide = h_wide(h, h->n);
   return h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0) |
-         (h->lanes == 0 && h->helper && wide ? 128 : 0) | (h->lanes == 0 && h->helper && nt_state(h, h->n) ? 256 : 0);
+         (h->lanes == 0 && h->helper && wide ? 128 : 0) | (h->lanes == 0 && h->helper && nt_state(h, h->n) ? 256 : 0) |
+         (h->lanes == 0 && h->helper && hd_form(h, h->n) ? 512 : 0);
 }
 
 int quad_seed(QuadHandle* h, uint64_t seed, void* stream) {
@@ -1831,9 +1864,21 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     hipLaunchKernelGGL((k_step_h<QUAD_ENV_HOVER, false, SP, HB, NT>), grid, blk2, 0, s, QD_KARGS);
 #define QD_LAUNCH_H(SP, HB) \
   if (nt) { QD_LAUNCH_H2(SP, HB, true) } else { QD_LAUNCH_H2(SP, HB, false) }
+#define QD_LAUNCH_HD(SP)                                                                        \
+  if (traj && ctbr)                                                                             \
+    hipLaunchKernelGGL((k_step_hd<QUAD_ENV_TRAJ, true, SP>), grid, blk2, 0, s, QD_KARGS);       \
+  else if (traj)                                                                                \
+    hipLaunchKernelGGL((k_step_hd<QUAD_ENV_TRAJ, false, SP>), grid, blk2, 0, s, QD_KARGS);      \
+  else if (ctbr)                                                                                \
+    hipLaunchKernelGGL((k_step_hd<QUAD_ENV_HOVER, true, SP>), grid, blk2, 0, s, QD_KARGS);      \
+  else                                                                                          \
+    hipLaunchKernelGGL((k_step_hd<QUAD_ENV_HOVER, false, SP>), grid, blk2, 0, s, QD_KARGS);
     const bool wide = h_wide(h, count);
     const bool nt = nt_state(h, count);
-    if (h->helper && !wide) {
+    if (h->helper && hd_form(h, count)) {
+      const dim3 grid(unsigned((int64_t(count) + 63) / 64)), blk2(128);
+      if (h->spec) { QD_LAUNCH_HD(true) } else { QD_LAUNCH_HD(false) }
+    } else if (h->helper && !wide) {
       const dim3 grid(unsigned((int64_t(count) + 63) / 64)), blk2(128);
       if (h->spec) { QD_LAUNCH_H(true, 64) } else { QD_LAUNCH_H(false, 64) }
     } else if (h->helper) {
@@ -1843,6 +1888,7 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
 #undef QD_LAUNCH_K
 #undef QD_LAUNCH_H
 #undef QD_LAUNCH_H2
+#undef QD_LAUNCH_HD
 #undef QD_KARGS
   } else {
     const dim3 grid(unsigned((int64_t(count) * G + BLOCK - 1) / BLOCK));
