@@ -171,6 +171,26 @@ def spec_mode(request, monkeypatch):
     return request.param
 
 
+def test_kernel_form_pins(monkeypatch):
+    """QUADENV_HD / QUADENV_NT / QUADENV_HBLOCK pin the size policy (quad_create reads them); k_step_hd
+    (bit 9) is only ever the 64-env nt launch: pinned on, it needs the nt policy and 64-env blocks."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    for v in ("QUADENV_HD", "QUADENV_NT", "QUADENV_HBLOCK", "QUADENV_LANES", "QUADENV_HELPER"):
+        monkeypatch.delenv(v, raising=False)
+    cases = ((1 << 22, dict(QUADENV_HD="0"), 32 | 256), (1 << 22, dict(QUADENV_NT="0"), 32),
+             (1 << 22, dict(QUADENV_HBLOCK="256"), 32 | 128 | 256), (4096, dict(QUADENV_HD="1"), 32),
+             (4096, dict(QUADENV_HD="1", QUADENV_NT="1"), 32 | 256 | 512),
+             (65536, dict(QUADENV_HD="1"), 32 | 128 | 256), (65536, dict(QUADENV_HD="1", QUADENV_HBLOCK="64"), 32 | 256 | 512))
+    for n, pins, form in cases:
+        for k, v in pins.items():
+            monkeypatch.setenv(k, v)
+        e = _env(n)
+        assert N.lib().quad_kernel_form(e._h) & ~16 == form, (n, pins)
+        e.close()
+        for k in pins:
+            monkeypatch.delenv(k)
+
+
 def test_kernel_form_selection(spec_mode):
     from uav_reinforcement_learning_control_amd import _native as N
     # 32: helper waves (k_step_h, the form at every size), + 128: in 256-env blocks (32,769 ..
