@@ -201,6 +201,8 @@ def _run_rank(args, rank, world, local_rank):
         res["rollout"] = _rollout_phase(env, args)
     if args.e2e_iters > 0:
         res["end_to_end"] = _end_to_end(env, args, world)
+        if world > 1:
+            res["end_to_end"]["shard_identity"] = _shard_identity(args, rank, world, dev)
     if rank == 0 and not args.no_configs:
         res["configs"] = {
             "config2_hover_4096": _kernel_rate(4096, "hover", None, dev, args.seed),
@@ -284,14 +286,20 @@ def _kstep_rate(n, steps, dev, seed) -> dict:
 
 def _end_to_end(env, args, world: int = 1) -> dict:
     """One full PPO iteration per SURVEY 8(d) config 3: rollout of n_steps (MFMA policy path) +
-    GAE + the SB3-schedule update (n_epochs x n_minibatches Adam steps on the rollout buffer)."""
+    GAE + the SB3-schedule update (n_epochs x n_minibatches Adam steps on the rollout buffer).
+    At world > 1 (config 4) also: the ranks as torch.distributed sees them, every gradient
+    all-reduce of the timed update HIP-event timed (allreduce_mean_) with its share of the optimizer
+    step, the same collective alone, and the episode statistics reduced over the ranks."""
     from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
     cfg = PPOConfig(n_steps=args.e2e_steps, n_epochs=args.e2e_epochs)
     m = PPO(env, cfg, seed=0)
-    m.collect_rollouts(use_graph=True)  # capture + warm (not timed)
+    first = m.collect_rollouts(use_graph=True)  # capture + warm (not timed)
+    first_stats = m._done_stats.tolist()  # the whole job's (reduced over ranks), before any update
     m.train(n_epochs=1, max_minibatches=2)
     torch.cuda.synchronize()
     t_roll = t_train = 0.0
+    if world > 1:
+        m.comm_events = []  # time every gradient all-reduce of the timed updates
     for _ in range(args.e2e_iters):
         rs = m.collect_rollouts(use_graph=True)
         t0 = time.perf_counter()
@@ -299,26 +307,96 @@ def _end_to_end(env, args, world: int = 1) -> dict:
         torch.cuda.synchronize()
         t_train += time.perf_counter() - t0
         t_roll += rs.seconds
+    comm = m.comm_stats() if world > 1 else None
     steps = args.e2e_iters * rs.env_steps * world  # every rank's envs (config 4 at N = 8)
     wall = t_roll + t_train
     if world > 1:  # the slowest rank sets the whole job's time
         t = torch.tensor([wall], dtype=torch.float64, device=env.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
-    out = {"world_size": world, "global_envs": env.num_envs * world,
+    opt_steps = max(1, cfg.n_epochs * m.n_minibatches_per_epoch())
+    ms_opt = 1e3 * t_train / args.e2e_iters / opt_steps
+    out = {"world_size": world, "n_ranks": dist.get_world_size() if world > 1 else 1,
+           "global_envs": env.num_envs * world,
            "grad_allreduce": "one flat fp32 bucket (37,001 params) per optimizer step" if world > 1 else None,
-           "n_steps": cfg.n_steps, "n_epochs": cfg.n_epochs, "minibatches_per_epoch": cfg.n_minibatches,
+           "n_steps": cfg.n_steps, "n_epochs": cfg.n_epochs, "minibatches_per_epoch": m.n_minibatches_per_epoch(),
            "minibatch": m.batch, "iterations": args.e2e_iters,
            "rollout_s": t_roll / args.e2e_iters, "train_s": t_train / args.e2e_iters,
            "update_path": "quad_ppo_grad (fused fwd+loss+bwd on MFMA) + quad_clip_adam"
            if m._learner is not None else "torch autograd",
-           "ms_per_optimizer_step": 1e3 * t_train / args.e2e_iters / max(1, cfg.n_epochs * cfg.n_minibatches),
-           "env_steps_per_s": steps / wall}
+           "ms_per_optimizer_step": ms_opt,
+           "env_steps_per_s": steps / wall,
+           "episodes_first_rollout": {"return_sum": first_stats[0], "length_sum": first_stats[1],
+                                      "count": int(first_stats[2]), "local_count": first.extra["local_episodes"],
+                                      "reduced_over_ranks": world > 1}}
+    if world > 1:
+        alone = _allreduce_alone(m)
+        out["allreduce"] = dict(
+            comm, what="HIP events on the optimizer step's stream around dist.all_reduce(SUM) of the "
+                       "148 KB bucket and work.wait() (ppo.allreduce_mean_), every optimizer step of the "
+                       "timed update(s)",
+            backend=dist.get_backend(), exposed_share_of_optimizer_step=comm["mean_us"] / (ms_opt * 1e3),
+            alone=alone)
     if m._learner is not None:
         out["learner_kernel"] = _learner_kernel(m)
     del m
     torch.cuda.empty_cache()
     return out
+
+
+def _allreduce_alone(m, reps: int = 50) -> dict:
+    """The gradient bucket's all-reduce by itself (no update around it): `reps` back-to-back
+    SUM all-reduces of a copy of the 148 KB bucket, HIP-event timed on the current stream."""
+    buf = m._flat.clone()
+    for _ in range(5):
+        dist.all_reduce(buf)
+    torch.cuda.synchronize()
+    dist.barrier()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dist.all_reduce(buf)
+    e1.record()
+    torch.cuda.synchronize()
+    return {"reps": reps, "us_per_allreduce": e0.elapsed_time(e1) * 1e3 / reps, "bytes": buf.numel() * 4}
+
+
+def _shard_identity(args, rank: int, world: int, dev, steps: int = 16) -> dict:
+    """Config 4's sharding check: rank r steps envs [r N, (r + 1) N) of the global
+    batch from a fresh handle (reset, then `steps` steps of the global-id-keyed random actions,
+    SB3 auto-reset on); its SHA-256 digest of every obs / reward / flag / terminal-obs output must
+    equal the digest rank 0 forms from the same rows of ONE handle of all world x N envs."""
+    import hashlib
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    n = args.envs
+
+    def run(e, lo, hi):
+        hs = [hashlib.sha256() for _ in range(lo, hi, n)]
+
+        def add(outs):
+            for j, a in enumerate(range(lo, hi, n)):
+                for t in outs:
+                    hs[j].update(t[a - lo:a - lo + n].contiguous().cpu().numpy().tobytes())
+        add([e.reset()])
+        for k in range(steps):
+            obs, rew, te, tr, inf = e.step(e.random_actions(k))
+            add([obs, rew, te, tr, inf["terminal_observation"]])
+        return [h.hexdigest() for h in hs]
+
+    mine = QuadVecEnv(n, env="hover", device=dev, seed=args.seed, env_id_base=rank * n)
+    d = run(mine, 0, n)[0]
+    mine.close()
+    got = [None] * world
+    dist.all_gather_object(got, d)
+    if rank != 0:
+        return {}
+    one = QuadVecEnv(world * n, env="hover", device=dev, seed=args.seed, env_id_base=0)
+    ref = run(one, 0, world * n)
+    one.close()
+    torch.cuda.empty_cache()
+    return {"steps": steps, "envs_per_rank": n, "one_handle_envs": world * n,
+            "rank_digests": [g[:16] for g in got], "one_handle_digests": [r[:16] for r in ref],
+            "all_equal": all(g == r for g, r in zip(got, ref))}
 
 
 def _learner_kernel(m) -> dict:

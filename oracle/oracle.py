@@ -105,6 +105,7 @@ def lib():
         L.oracle_mj_forward.argtypes = [C.POINTER(OracleOpt), dp, dp, dp, dp, dp, dp, dp, dp]
         L.oracle_quat_to_euler.argtypes = [dp, dp]
         L.oracle_euler_to_quat.argtypes = [dp, dp]
+        L.oracle_quat_to_euler_batch.argtypes = [dp, C.c_int32, dp]
         L.oracle_get_obs.argtypes = [C.POINTER(OracleCfg), C.POINTER(OracleEnv), fp]
         L.oracle_relpos_obs.argtypes = [C.POINTER(OracleEnv), fp, fp]
         L.oracle_env_reset.argtypes = [C.POINTER(OracleCfg), C.POINTER(OracleEnv), fp, fp, fp]
@@ -187,6 +188,14 @@ def quat_to_euler(q_wxyz):
     q = np.ascontiguousarray(q_wxyz, dtype=np.float64)
     e = np.zeros(3)
     lib().oracle_quat_to_euler(_dp(q), _dp(e))
+    return e
+
+
+def quat_to_euler_batch(q_wxyz):
+    """[n, 4] wxyz quaternions -> [n, 3] float64 scipy as_euler('xyz') angles (oracle_quat_to_euler)."""
+    q = np.ascontiguousarray(np.asarray(q_wxyz, np.float64).reshape(-1, 4))
+    e = np.zeros((q.shape[0], 3))
+    lib().oracle_quat_to_euler_batch(_dp(q), q.shape[0], _dp(e))
     return e
 
 

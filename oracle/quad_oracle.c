@@ -535,6 +535,12 @@ void oracle_quat_to_euler(const double q_wxyz[4], double e[3]) {
   }
 }
 
+/* oracle_quat_to_euler over n quaternions (wxyz rows): the tests' Euler angles of the kernel's own
+ * post-step quaternions (tests/test_gpu_parity.py euler_of_quat) */
+void oracle_quat_to_euler_batch(const double* q_wxyz, int32_t n, double* e) {
+  for (int32_t i = 0; i < n; i++) oracle_quat_to_euler(q_wxyz + 4 * (size_t)i, e + 3 * (size_t)i);
+}
+
 void oracle_euler_to_quat(const double e[3], double q_wxyz[4]) {
   /* from_euler('xyz'): extrinsic composition q = qz * (qy * qx), elements xyzw */
   double res[4] = {sin(e[0] / 2), 0, 0, cos(e[0] / 2)};

@@ -286,25 +286,31 @@ def test_fused_grad_rejects_bad_arguments():
     assert L.quad_ppo_grad(None, None, None, None, 0, None) == N.QUAD_EINVAL
 
 
-def test_ppo_train_fused_matches_torch_update(learner_form):
-    """One PPO.train pass (2 minibatches) with the fused gradient vs the torch loss. Adam's first
-    steps move each parameter by ~lr * sign(g), so a gradient element within fp32 noise of zero
-    can move either way: allow that (<= 2 lr per step) on a small fraction of the elements, and
-    fp32 noise elsewhere."""
+@pytest.mark.parametrize("batch_size", [None, 5000, 16384 + 5])
+def test_ppo_train_fused_matches_torch_update(learner_form, batch_size):
+    """One PPO.train pass with the fused gradient vs the torch loss: 2 equal minibatches; SB3's
+    ragged partition (batch_size 5000 over 16,384 rows: three full minibatches and a short fourth,
+    RolloutBuffer.get); and batch_size > the buffer (one minibatch of every row; the epoch
+    statistics launch cannot serve it, so the gradient's own pre-pass does). Adam's first steps move
+    each parameter by ~lr * sign(g), so a gradient element within fp32 noise of zero can move either
+    way: allow that (<= 2 lr per step) on a small fraction of the elements, and fp32 noise elsewhere."""
     from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
     from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
     outs = []
     for fused in (True, False):
         env = QuadVecEnv(1024, env="hover", device="cuda:0", seed=3)
-        cfg = PPOConfig(n_steps=16, n_minibatches=2, n_epochs=1, fused_update=fused)
+        cfg = PPOConfig(n_steps=16, n_minibatches=2, n_epochs=1, fused_update=fused, batch_size=batch_size)
         algo = PPO(env, cfg, seed=11)
+        assert (algo._learner is not None) == fused
         algo.collect_rollouts()
         torch.manual_seed(5)  # same epoch permutation
         st = algo.train()
         outs.append(([p.detach().clone() for p in algo.policy.parameters()], st))
         env.close()
     (pa, sa), (pb, sb) = outs
-    lr, steps = PPOConfig().learning_rate, 2
+    steps = {None: 2, 5000: 4, 16384 + 5: 1}[batch_size]
+    assert sa["n"] == sb["n"] == steps
+    lr = PPOConfig().learning_rate
     d = torch.cat([(a - b).abs().reshape(-1) for a, b in zip(pa, pb)])
     assert d.max().item() <= 2 * lr * steps + 1e-6
     assert (d > 1e-6).float().mean().item() < 0.01, f"{(d > 1e-6).sum().item()} of {d.numel()} differ"

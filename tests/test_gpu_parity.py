@@ -27,34 +27,47 @@ def _env(n, env="hover", wrapper=None, **kw):
     return QuadVecEnv(n, env=env, wrapper=wrapper, device="cuda:0", **kw)
 
 
-def parity_ok(got, ref, pre=None, rtol=1e-5, atol=1e-6, extra=0.0):
+def parity_ok(got, ref, pre=None, rtol=1e-5, atol=1e-6):
     got = np.asarray(got, np.float64); ref = np.asarray(ref, np.float64)
     scale = np.abs(ref) if pre is None else np.maximum(np.abs(ref), np.abs(np.asarray(pre, np.float64)))
     both_nan = np.isnan(got) & np.isnan(ref)
-    return np.all(both_nan | (np.abs(got - ref) <= rtol * scale + atol + extra), axis=-1)
+    return np.all(both_nan | (np.abs(got - ref) <= rtol * scale + atol), axis=-1)
 
 
-# Euler angles near gimbal lock (DESIGN.md section 4). scipy's as_euler('xyz') of a quaternion has
-# roll and yaw individually ill-conditioned as |pitch| -> pi/2: d(roll), d(yaw) ~ |dq| / cos(pitch),
-# while roll - sign(pitch) yaw stays well-conditioned. The state is float32 (a design decision), so
-# the quaternion a step produces carries ~1 ulp of rounding whatever the implementation: rounding the
-# float64 oracle's own post-step quaternion to float32 moves roll / yaw by up to 1.2e-4 at
-# cos(pitch) = 3e-4 (tests/test_gpu_parity_full.py rows). Roll / yaw (state12[3], [5]; obs[3], [5]
-# scaled by the normalization) get EULER_ULPS float32 ulps of the quaternion amplified by
-# 1 / cos(pitch) on top of the bar, and the well-conditioned combination is held to the plain bar.
-EULER_ULPS = 8
+# The Euler columns (state12[3:6], obs[3:6]). scipy's as_euler('xyz') of a
+# quaternion has roll and yaw individually ill-conditioned as |pitch| -> pi/2: d(roll), d(yaw) ~
+# |dq| / cos(pitch), while roll - sign(pitch) yaw stays well-conditioned. The state is float32 (a
+# design decision), so the quaternion a step produces carries ~1 ulp of rounding whatever the
+# implementation: rounding the float64 oracle's own post-step quaternion to float32 moves roll / yaw
+# by up to 1.2e-4 at cos(pitch) = 3e-4. So the Euler columns are pinned in parts, each at the plain
+# bar |d| <= 1e-5 |ref| + 1e-6 with no extra tolerance: (i) the post-step quaternion qpos[3:7]
+# against the oracle's; (ii) state12[3:6] and obs[3:6] against the oracle's float64 quat -> Euler
+# (+ normalize) OF THE KERNEL'S OWN float32 QUATERNION (the conversion's arithmetic, at any pitch);
+# (iii) roll - sign(pitch) yaw against the oracle's (euler_combination_ok).
+NON_EULER = [0, 1, 2, 6, 7, 8, 9, 10, 11]
 
 
-def euler_slack(ref_s12, obs_span=None):
-    """[n, 12] extra tolerance for the Euler columns of state12 (obs_span None) or of the
-    normalized observation (obs_span = obs_high - obs_low, [12]), from the oracle's pitch."""
-    ref_s12 = np.atleast_2d(np.asarray(ref_s12, np.float64))
-    c = np.maximum(np.abs(np.cos(ref_s12[:, 4])), 1e-6)
-    x = np.zeros(ref_s12.shape)
-    k = EULER_ULPS * 2.0 ** -24 / c
-    for j in (3, 5):
-        x[:, j] = k if obs_span is None else k * 2.0 / float(obs_span[j])
-    return x
+def euler_of_quat(qpos):
+    """float32 scipy Euler angles of the quaternions qpos[:, 3:7] (the oracle's float64 conversion)."""
+    return O.quat_to_euler_batch(np.atleast_2d(np.asarray(qpos, np.float64))[:, 3:7]).astype(np.float32)
+
+
+def obs_euler_of_quat(qpos):
+    """obs[3:6] of those angles: normalize (utils/normalization.py:7-17) in float32, NumPy's order."""
+    e = euler_of_quat(qpos)
+    lo, hi = OBS_LOW[3:6], OBS_HIGH[3:6]
+    return (np.float32(2) * (e - lo)) / (hi - lo) - np.float32(1)
+
+
+def euler_ok(got_s12, got_obs, got_qpos, ref_qpos):
+    """Per row: (i) the quaternion vs the oracle's and (ii) the Euler columns of state12 (and of obs,
+    unless got_obs is None) vs the conversion of the kernel's own quaternion, at the plain bar."""
+    gq = np.atleast_2d(got_qpos)
+    ok = parity_ok(gq[:, 3:7], np.atleast_2d(ref_qpos)[:, 3:7])
+    ok &= parity_ok(np.atleast_2d(got_s12)[:, 3:6], euler_of_quat(gq))
+    if got_obs is not None:
+        ok &= parity_ok(np.atleast_2d(got_obs)[:, 3:6], obs_euler_of_quat(gq))
+    return ok
 
 
 def euler_combination_ok(got_s12, ref_s12, rtol=1e-5, atol=1e-6):
@@ -70,6 +83,7 @@ def euler_combination_ok(got_s12, ref_s12, rtol=1e-5, atol=1e-6):
 
 _OC = O.default_cfg(O.ENV_HOVER, O.WRAP_NONE)
 OBS_SPAN = np.array(_OC.obs_high[:], np.float64) - np.array(_OC.obs_low[:], np.float64)  # same for both kinds
+OBS_LOW, OBS_HIGH = np.array(_OC.obs_low[:], np.float32), np.array(_OC.obs_high[:], np.float32)
 CANCEL = 0.1  # the documented class: |ref| <= CANCEL |pre|, a step that removed >= 90 % of the operand
 
 
@@ -229,16 +243,18 @@ def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap, kernel
     g = _gpu_step(env, st, acts)
     ref = _oracle_step(kind, wrap, st, acts)
     bad = []
+    eul = euler_ok(g["state12"], g["obs"], g["qpos"], np.stack([o["qpos"] for o in ref]))
     for i, o in enumerate(ref):
         ok = (g["terminated"][i] == o["terminated"] and g["truncated"][i] == o["truncated"]
               and g["step_count"][i] == st["step_count"][i] + 1
-              and parity_ok(g["obs"][i], o["obs"], extra=euler_slack(o["state12"], OBS_SPAN)[0])
+              and parity_ok(g["obs"][i][NON_EULER], o["obs"][NON_EULER])
               and parity_ok(g["reward"][i], o["reward"])
               and parity_ok(g["voltage"][i], o["voltage"])
               and parity_ok(g["qpos"][i], o["qpos"], st["qpos"][i])
               and parity_ok(g["qvel"][i], o["qvel"], st["qvel"][i])
               and parity_ok(g["motor"][i], o["motor_commands"])
-              and parity_ok(g["state12"][i], o["state12"], _pre12(st, i), extra=euler_slack(o["state12"])[0])
+              and parity_ok(g["state12"][i][NON_EULER], o["state12"][NON_EULER], _pre12(st, i)[NON_EULER])
+              and eul[i]
               and euler_combination_ok(g["state12"][i], o["state12"]).all()
               and parity_ok(g["rate_int"][i], o["rate_int"], st["rate_int"][i], atol=1e-9))
         if not ok:

@@ -29,8 +29,8 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from test_gpu_parity import (OBS_SPAN, _random_states, euler_combination_ok, euler_slack, operand_only,
-                             parity_ok)
+from test_gpu_parity import (NON_EULER, _random_states, euler_combination_ok, euler_ok, obs_euler_of_quat,
+                             operand_only, parity_ok)
 
 pytestmark = pytest.mark.gpu
 
@@ -100,11 +100,15 @@ def _check_rows(g, ref, st, rows, what):
         elif k == "state12":
             pre = np.concatenate([st["qpos"][rows][:, :3], np.zeros((len(rows), 3), np.float32),
                                   st["qvel"][rows][:, :6]], 1)
-            note(k, parity_ok(g["state12"][rows], ref["state12"][rows], pre, extra=euler_slack(ref["state12"][rows])))
+            note(k, parity_ok(g["state12"][rows][:, NON_EULER], ref["state12"][rows][:, NON_EULER], pre[:, NON_EULER]))
+            note("euler", euler_ok(g["state12"][rows], None, g["qpos"][rows], ref["qpos"][rows]))
             note("roll-yaw", euler_combination_ok(g["state12"][rows], ref["state12"][rows]))
         elif k == "obs":
-            # (reset rows carry the reset obs in both and are compared bit-exactly elsewhere)
-            note(k, parity_ok(g["obs"][rows], ref["obs"][rows], extra=euler_slack(ref["state12"][rows], OBS_SPAN)))
+            # (reset rows carry the reset obs in both and are compared bit-exactly elsewhere); the
+            # Euler columns against the conversion of the kernel's own quaternion (test_gpu_parity)
+            note(k, parity_ok(g["obs"][rows][:, NON_EULER], ref["obs"][rows][:, NON_EULER]))
+            note("obs-euler", parity_ok(g["obs"][rows][:, 3:6], obs_euler_of_quat(g["qpos"][rows])))
+            note("quat", parity_ok(g["qpos"][rows][:, 3:7], ref["qpos"][rows][:, 3:7]))
         else:
             gk, rk = g[k][rows], ref[k][rows]
             if gk.ndim == 1:

@@ -5,6 +5,8 @@ collect_rollouts calls env.step(clipped_actions) -> (obs, rewards, dones, infos)
 infos[i]["terminal_observation"] / ["TimeLimit.truncated"] / ["episode"] (SB3 DummyVecEnv +
 Monitor semantics, restated in the facade's docstring).
 """
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -35,6 +37,7 @@ def test_sb3_facade_matches_quadvecenv(wrapper):
     assert np.array_equal(o.view(np.uint32), ref.reset().cpu().numpy().view(np.uint32))
     ep_ret = np.zeros(n)
     ep_len = np.zeros(n, np.int64)
+    t_built = venv._t_start
     finished = truncs = 0
     for t in range(T):
         acts = ref.random_actions(t)
@@ -59,7 +62,9 @@ def test_sb3_facade_matches_quadvecenv(wrapper):
                 inf = infos[i]
                 assert np.array_equal(inf["terminal_observation"], tobs[i]), (t, i)
                 assert inf["TimeLimit.truncated"] == bool(tl[i])
-                assert inf["episode"]["r"] == ep_ret[i] and inf["episode"]["l"] == ep_len[i]
+                # Monitor: "r" = round(sum of the rewards, 6), "t" seconds since construction
+                assert inf["episode"]["r"] == round(float(ep_ret[i]), 6) and inf["episode"]["l"] == ep_len[i]
+                assert 0.0 <= inf["episode"]["t"] <= time.time() - t_built + 1e-6
                 truncs += int(tl[i])
             else:
                 assert infos[i] == {}

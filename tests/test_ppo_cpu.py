@@ -117,6 +117,14 @@ def _worker_body(rank, world, port, q):
     assert torch.equal(bucket, local)
     allreduce_mean_(params, bucket, world)
     assert _bucket_bound(params, bucket) and torch.equal(bucket, avg)
+    # broadcast_parameters_: a rank-dependent initialization ends equal to rank 0's
+    from uav_reinforcement_learning_control_amd.ppo.ppo import broadcast_parameters_
+    torch.manual_seed(7 + rank)
+    r = ActorCritic()
+    broadcast_parameters_(list(r.parameters()), 0)
+    torch.manual_seed(7)
+    r0 = ActorCritic()
+    assert all(torch.equal(a, b) for a, b in zip(r.parameters(), r0.parameters()))
     q.put((rank, local.numpy(), avg.numpy()))
     dist.destroy_process_group()
 
@@ -164,3 +172,14 @@ def test_cpu_ppo_baseline_runs_the_reference_loop_shape():
     assert r["cores"] == 1 and r["kind"] == "port" and r["value"] > 0
     assert "16 oracle envs" in r["sample"] and "2560 Adam steps" in r["sample"]
     assert torch.get_num_threads() >= 1  # the thread count is restored
+
+
+def test_minibatch_partition_is_sb3s():
+    """SB3 RolloutBuffer.get(batch_size) slices indices[start:start + batch_size] for start < total:
+    ceil(total / batch) minibatches, the last one short, one minibatch when batch_size >= total."""
+    from uav_reinforcement_learning_control_amd.ppo.ppo import n_minibatches
+    for total, batch in ((16384, 8192), (16384, 5000), (16384, 16389), (1, 128), (16 * 1024, 128), (10, 3)):
+        starts = list(range(0, total, batch))
+        assert n_minibatches(total, batch) == len(starts), (total, batch)
+        sizes = [min(total, s + batch) - s for s in starts]
+        assert sum(sizes) == total

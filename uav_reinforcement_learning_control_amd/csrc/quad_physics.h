@@ -644,11 +644,19 @@ QD_HD void physics_step(const PhysConsts<T>& c, EnvRegs<T>& e, const double Fin[
 
 // ---------------------------------------------------------------------------------------------
 // scipy Rotation.from_quat(xyzw).as_euler('xyz') (utils/state.py:42): Bernardes & Viollet
+// from_quat's normalization is left out in float32: every angle below is a function of ratios
+// (atan2, the ratio of the two hypots), so the scale of q cancels, and the raw components keep the
+// terms that vanish at gimbal lock exact -- a = qw - qy and b = qx + qz of nearly equal / opposite
+// operands are exact by Sterbenz, while the components of a float32-normalized q each carry a
+// rounding that a / b, ~cos(pitch) / 2 there, amplified into roll / yaw by 1 / cos(pitch) (3.5e-4 rad
+// at cos(pitch) = 3.3e-4). The float64 instantiation keeps scipy's normalize-first sequence.
 template <typename T>
 QD_HD void quat_to_euler(const T qin[4], T e[3]) {
-  T q[4] = {qin[0], qin[1], qin[2], qin[3]};
-  const T inv = q_rsqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  const T qw = q[0] * inv, qx = q[1] * inv, qy = q[2] * inv, qz = q[3] * inv;
+  T qw = qin[0], qx = qin[1], qy = qin[2], qz = qin[3];
+  if constexpr (sizeof(T) == 8) {
+    const T inv = q_rsqrt(qw * qw + qx * qx + qy * qy + qz * qz);
+    qw *= inv; qx *= inv; qy *= inv; qz *= inv;
+  }
   const T a = qw - qy, b = qx + qz, c = qy + qw, d = qz - qx;
   const T PI = T(3.14159265358979323846);
   T mid = T(2) * q_atan2(q_hypot(c, d), q_hypot(a, b));

@@ -103,18 +103,6 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, size_t row, 
   b4[2] = make_float4(v[8], v[9], v[10], v[11]);
 }
 
-// QD_ROLL_OVL: 1 = the env step in the critic's issue gaps, 0 = after both nets (the round-3
-// order; default). Same bits (tools/env_digest.py). Measured (round 4, tools/rollout_variants.py,
-// 65,536 envs, T = 64): 27.63 / 27.74 us per step with the overlap vs 27.38 / 27.65 without -- the
-// env step is ~2.4 us of the step (QD_ROLL_NOENV 25.28) and its VALU does not hide in the critic's
-// steps, which are not matrix-pipe-bound (the MLPs run at ~0.5 of their MFMA floor)
-#if defined(QD_ROLL_NOENV) || defined(QD_ROLL_NOCRITIC) || defined(QD_ROLL_NOMLP)
-#undef QD_ROLL_OVL
-#define QD_ROLL_OVL 0  // the cost-ablation builds time the round-3 order
-#endif
-#ifndef QD_ROLL_OVL
-#define QD_ROLL_OVL 0
-#endif
 // QD_ROLL_ALP: the actor's W2 pieces from LDS (policy_net.h stage_pieces / LP_SPLIT), the
 // critic's from L2; 0 = both from L2 (round 3). Same bits.
 #ifndef QD_ROLL_ALP
@@ -140,49 +128,6 @@ __device__ __forceinline__ void sample_action(const RollArgs& a, const KParams& 
     ac[k] = fminf(fmaxf(act[k], -1.f), 1.f);
   }
 }
-
-// env_step (quad_physics.h) as pieces for the critic's layer-2 steps g: the same calls in the same
-// order (env_control, mj_checkPos/Vel, forward_base's base part and four props, the motor wrench,
-// physics_finish, the observation, reward and flags), so the same bits
-template <bool CTBR>
-struct StepCo {
-  Ctl<float> c;
-  bool zero;
-  float qn[4];
-  BaseAcc<float> b;
-  __device__ __forceinline__ void chunk(const KConsts<float>& K, EnvRegs<float>& e, const float (&ac)[ACT],
-                                        StepRes& r, int g) {
-    const PhysConsts<float>& ph = K.ph;
-    if (g == 1) {
-      c = env_control<float, CTBR>(K, e.volt, e.w, e.rint, ac);
-      e.volt = c.volt;
-    } else if (g == 3) {
-      const bool bad = check_state(e);  // mj_checkPos / mj_checkVel
-      zero = bad || any_bad_ctrl<float>(c.F);
-#pragma unroll
-      for (int j = 0; j < 4; j++) qn[j] = e.q[j];
-      normalize4(qn);
-    } else if (g == 5) {
-      forward_base_begin(ph, qn, e.v, e.w, b);
-    } else if (g == 7 || g == 9 || g == 11 || g == 13) {
-      const int pr = (g - 7) / 2;
-      forward_prop(ph, pr, e.th[pr], e.w, e.s[pr], b);
-    } else if (g == 16) {
-      const Wrench<float> m = wrench_of<float, true>(ph, c.F, zero);  // F = clip(., 0, max) * vs >= 0
-      physics_finish<float, true>(ph, e, qn, b.a, m);
-    } else if (g == 20) {
-      e.step += 1;  // env_post
-      observe(K, e, r.obs, r.state12);
-    } else if (g == 23) {
-      r.reward = reward_of<float>(r.state12, e.target);
-      r.term = terminated_of(K, r.state12);
-      r.trunc = e.step >= K.max_steps;
-#pragma unroll
-      for (int j = 0; j < 4; j++) r.motor[j] = float(c.F[j]);
-      r.vscale = float(c.vs);
-    }
-  }
-};
 
 // NT = 2: 4 waves (one per SIMD), wave w owns envs 64w .. 64w + 63 = its two MFMA tiles.
 // NT = 1: 8 waves (two per SIMD), wave w owns the 32 envs 32w .. 32w + 31 = one tile; lanes l and
@@ -242,30 +187,6 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
 #pragma unroll
       for (int k = 0; k < ACT; k++) mean[j][k] = xb[j][k];
     }
-#elif QD_ROLL_OVL
-    // the actor, then the action; the env step of that action runs in the critic's layer-2 issue
-    // gaps (the critic's value only goes to the buffer): ~1.2 k VALU that ran after both nets
-    StepRes r;
-    float act[ACT], ac[ACT], lp = 0.f;
-    {
-      P3 xp[NT];
-#pragma unroll
-      for (int j = 0; j < NT; j++) xp[j] = split8(xb[j]);
-      const NetOff oa = net_off(0, packed, 0), oc = net_off(ACTOR_F, packed, 1);
-      Pipe<NT> pst;
-      pipe_start<NT, bool(QD_ROLL_ALP)>(lds, oa, xp, pst);
-      net_core<ACT, NT, true, 0, bool(QD_ROLL_ALP)>(lds, oa, oc, xp, pst, mean);
-      sample_action<NT>(a, p, i, t, h, mean, sd, lstd, act, ac, lp);
-      StepCo<CTBR> co;
-      net_core<1, NT, false, 32>(lds, oc, oc, xp, pst, val, [&](int g) { co.chunk(K, e, ac, r, g); });
-    }
-    if (owner) {
-      store_row(a.obs_copy, row, ob);
-      reinterpret_cast<float4*>(a.actions)[row] = make_float4(act[0], act[1], act[2], act[3]);
-      a.log_prob[row] = lp;
-      a.value[row] = (NT == 2 && h) ? val[NT - 1][0] : val[0][0];
-      a.starts[row] = ls;
-    }
 #else
 #if defined(QD_ROLL_NOCRITIC)
     net_forward<ACT, NT>(lds, packed, xb, mean);
@@ -275,7 +196,6 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
     net_forward2<NT, bool(QD_ROLL_ALP)>(lds, packed, xb, mean, val);
 #endif
 #endif
-#if defined(QD_ROLL_NOMLP) || !QD_ROLL_OVL
     float act[ACT], ac[ACT], lp = 0.f;
     sample_action<NT>(a, p, i, t, h, mean, sd, lstd, act, ac, lp);
     if (owner) {
@@ -293,7 +213,6 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
     r.reward = ac[0]; r.term = false; r.trunc = false;
 #else
     env_step<float, CTBR>(K, e, ac, r);
-#endif
 #endif
     const bool done = r.term || r.trunc;
     // ---- TimeLimit bootstrap: r += gamma V(terminal_obs) (critic only if the wave holds one)

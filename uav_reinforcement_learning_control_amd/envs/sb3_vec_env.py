@@ -57,7 +57,7 @@ class QuadSB3VecEnv:
         self._actions: Optional[torch.Tensor] = None
         self._ep_ret = torch.zeros(self.num_envs, dtype=torch.float64, device=env.device)
         self._ep_len = torch.zeros(self.num_envs, dtype=torch.int64, device=env.device)
-        self._t_start = time.time()
+        self._t_start = time.time()  # Monitor.__init__ sets t_start once; reset() keeps it
         self._seeds: List[Optional[int]] = [None] * self.num_envs
         self.closed = False
 
@@ -72,7 +72,6 @@ class QuadSB3VecEnv:
         self._seeds = [None] * self.num_envs
         self._ep_ret.zero_()
         self._ep_len.zero_()
-        self._t_start = time.time()
         self.reset_infos = [{} for _ in range(self.num_envs)]
         return self._out(obs)
 
@@ -104,7 +103,7 @@ class QuadSB3VecEnv:
         elapsed = round(time.time() - self._t_start, 6)
         for k, i in enumerate(d_np.tolist()):
             infos[i] = {"TimeLimit.truncated": bool(tl_h[k]), "terminal_observation": tobs_h[k],
-                        "episode": {"r": float(r_h[k]), "l": int(l_h[k]), "t": elapsed}}
+                        "episode": {"r": round(float(r_h[k]), 6), "l": int(l_h[k]), "t": elapsed}}
         if self.full_info:  # HoverEnv's own info keys for every env (rows of the batched tensors)
             extra = {k: v.cpu().numpy() for k, v in inf.items()
                      if k not in ("terminal_observation", "TimeLimit.truncated")}

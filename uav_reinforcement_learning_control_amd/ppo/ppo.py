@@ -57,6 +57,18 @@ class PPOConfig:
     fused_update: bool = True             # minibatch gradient on MFMA (ppo/learner.py, quad_ppo_grad)
 
 
+# quad_ppo_adv_stats_epoch's grid y limit is 65,535; its [n, 512] float64 output is 4 KB per
+# minibatch, so the one-launch statistics are used up to 4,096 minibatches per epoch (16 MB)
+EPOCH_STATS_MAX_MINIBATCHES = 4096
+
+
+def n_minibatches(total: int, batch: int) -> int:
+    """SB3 RolloutBuffer.get(batch_size): slices indices[start:start + batch_size] for start = 0,
+    batch_size, ... < total -- ceil(total / batch) minibatches, the last one short when batch_size
+    does not divide the buffer, one minibatch of every row when batch_size >= total."""
+    return max(1, -(-int(total) // int(batch)))
+
+
 def epoch_permutation(total: int, device: torch.device) -> torch.Tensor:
     """The epoch's minibatch order (SB3 PPO.train: np.random.permutation(buffer_size)). On a ROCm
     GPU it is quad_permutation -- a keyed Feistel bijection of [0, total) computed one index per
@@ -109,14 +121,18 @@ def _bucket_bound(params, flat: torch.Tensor) -> bool:
     return True
 
 
-def allreduce_mean_(params, flat: torch.Tensor, world: int, between: Optional[Callable[[], None]] = None) -> None:
+def allreduce_mean_(params, flat: torch.Tensor, world: int, between: Optional[Callable[[], None]] = None,
+                    timing: Optional[list] = None) -> None:
     """Average the gradients of `params` over ranks with ONE all_reduce of a flat fp32 bucket:
     SUM, then a division by the world size -- the same two ops on RCCL and on gloo, so the gloo
     tests exercise exactly what the GPU job runs. With the .grad tensors bound to the bucket
     (bind_grad_bucket) the collective runs in place; otherwise (a caller replaced a .grad) they are
     copied in and out. `between`, if given, is called while the collective is in flight (it must
     not touch the bucket): on RCCL its launches overlap the all-reduce (work.wait() only makes the
-    current stream wait on the communication stream)."""
+    current stream wait on the communication stream). `timing`, if given (a list, CUDA tensors),
+    receives a pair of HIP events recorded on the current stream before the collective is issued
+    and after work.wait(): their interval is the time the step's own stream is held by the
+    all-reduce (the exposed communication of this optimizer step; PPO.comm_stats)."""
     bound = _bucket_bound(params, flat)
     if not bound:
         off = 0
@@ -124,16 +140,37 @@ def allreduce_mean_(params, flat: torch.Tensor, world: int, between: Optional[Ca
             k = p.numel()
             flat[off:off + k].copy_(p.grad.reshape(-1))
             off += k
+    ev = None
+    if timing is not None and flat.is_cuda:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True)
     if between is not None:
         between()
     work.wait()
+    if ev is not None:
+        ev[1].record()
+        timing.append(ev)
     flat.div_(world)
     if not bound:
         off = 0
         for p in params:
             k = p.numel()
             p.grad.copy_(flat[off:off + k].view_as(p))
+            off += k
+
+
+def broadcast_parameters_(params, src: int = 0) -> None:
+    """Every rank starts from rank `src`'s parameters (one broadcast of a flat copy): the ranks'
+    identical initialization does not rest on each rank seeding torch the same way before the
+    policy is built."""
+    flat = torch.cat([p.detach().reshape(-1) for p in params])
+    dist.broadcast(flat, src)
+    off = 0
+    with torch.no_grad():
+        for p in params:
+            k = p.numel()
+            p.copy_(flat[off:off + k].view_as(p))
             off += k
 
 
@@ -158,6 +195,8 @@ class PPO:
         self.obs_dim = int(getattr(env, "obs_dim", 12))
         self.policy = (policy or ActorCritic(self.obs_dim, 4, self.cfg.net_arch)).to(self.device)
         self.params = [p for p in self.policy.parameters()]
+        if self.world > 1:
+            broadcast_parameters_(self.params, 0)
         self.opt = torch.optim.Adam(self.params, lr=self.cfg.learning_rate, eps=self.cfg.adam_eps,
                                     fused=self.device.type == "cuda")  # one kernel per step
         torch.manual_seed(seed + 1000 * (dist.get_rank() if self.world > 1 else 0))
@@ -210,6 +249,7 @@ class PPO:
         self._t_host = 0  # running step counter of the one-launch path (keys the action noise)
         self._cursor_resume = None  # the two-launch path's noise counter after load_state_dict
         self._noise_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5851F42D4C957F2D) & (2**64 - 1)
+        self.comm_events: Optional[list] = None  # a list: time each gradient all-reduce (comm_stats)
 
     # ------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -308,13 +348,7 @@ class PPO:
         last_v = self._bootstrap_value()
         gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
             cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
-        torch.cuda.synchronize(self.device)
-        steps = cfg.n_steps * env.num_envs
-        self.num_timesteps += steps * self.world
-        ret_sum, len_sum, c = self._done_stats.tolist()
-        return RolloutStats(episodes=int(c), mean_return=ret_sum / c if c else float("nan"),
-                            mean_length=len_sum / c if c else float("nan"),
-                            env_steps=steps, seconds=time.perf_counter() - t0)
+        return self._rollout_stats(t0)
 
     @torch.no_grad()
     def _collect_one_launch(self) -> RolloutStats:
@@ -338,19 +372,45 @@ class PPO:
         last_v = self._bootstrap_value()
         gae(self.buf_rew, self.buf_val, self.buf_start, last_v, self.last_start,
             cfg.gamma, cfg.gae_lambda, self.buf_adv, self.buf_ret)
+        return self._rollout_stats(t0)
+
+    def _rollout_stats(self, t0: float) -> RolloutStats:
+        """Monitor-style statistics of the episodes that finished during the rollout, over every
+        rank's envs (one small all-reduce per rollout -- the sums of returns, lengths
+        and counts, float64), so the logged mean return is the whole job's, not rank 0's shard."""
+        local = self._done_stats.clone()
+        if self.world > 1:
+            dist.all_reduce(self._done_stats, op=dist.ReduceOp.SUM)
         torch.cuda.synchronize(self.device)
-        steps = cfg.n_steps * env.num_envs
+        steps = self.cfg.n_steps * self.env.num_envs
         self.num_timesteps += steps * self.world
         ret_sum, len_sum, c = self._done_stats.tolist()
         return RolloutStats(episodes=int(c), mean_return=ret_sum / c if c else float("nan"),
                             mean_length=len_sum / c if c else float("nan"),
-                            env_steps=steps, seconds=time.perf_counter() - t0)
+                            env_steps=steps, seconds=time.perf_counter() - t0,
+                            extra={"local_episodes": int(local[2].item()), "ranks": self.world})
+
+    def comm_stats(self, clear: bool = True) -> Optional[dict]:
+        """The gradient all-reduces timed since comm_events was set to a list (HIP events around the
+        collective and work.wait(), allreduce_mean_): count, mean / median / max microseconds of the
+        time each held the optimizer step's stream. None when nothing was timed."""
+        if not self.comm_events:
+            return None
+        torch.cuda.synchronize(self.device)
+        us = sorted(a.elapsed_time(b) * 1e3 for a, b in self.comm_events)
+        if clear:
+            self.comm_events = []
+        return {"count": len(us), "mean_us": sum(us) / len(us), "median_us": us[len(us) // 2], "max_us": us[-1]}
 
     def _bootstrap_value(self) -> torch.Tensor:
         """V(last_obs) for GAE: the MFMA policy kernel when fused (batch-independent rows), else torch."""
         if self._fp is not None:
             return self._fp.value(self.last_obs, self._last_v, self._act_env)
         return self.policy.value(self.last_obs)
+
+    def n_minibatches_per_epoch(self) -> int:
+        """Optimizer steps per epoch of train(): SB3's partition of the rollout buffer."""
+        return n_minibatches(self.cfg.n_steps * self.env.num_envs, self.batch)
 
     # ------------------------------------------------------------------------------------
     def train(self, n_epochs: Optional[int] = None, max_minibatches: Optional[int] = None) -> dict:
@@ -362,7 +422,7 @@ class PPO:
         adv_all = self.buf_adv.view(total)
         ret = self.buf_ret.view(total)
         B = self.batch
-        nmb = max(1, total // B)
+        nmb = n_minibatches(total, B)
         stats = dict(pg_loss=0.0, vf_loss=0.0, entropy=0.0, clip_fraction=0.0, n=0)
         acc = torch.zeros(4, dtype=torch.float64, device=self.device)
         epochs = n_epochs if n_epochs is not None else cfg.n_epochs
@@ -374,13 +434,13 @@ class PPO:
             for m in range(nmb):
                 if max_minibatches is not None and done >= max_minibatches:
                     break
-                idx = perm[m * B:(m + 1) * B]
+                idx = perm[m * B:min(total, (m + 1) * B)]
                 loss, pg, vf, ent, cf = ppo_loss(pol, obs[idx], act[idx], logp_old[idx],
                                                  adv_all[idx], ret[idx], cfg)
                 self.opt.zero_grad(set_to_none=False)
                 loss.backward()
                 if self.world > 1:
-                    allreduce_mean_(self.params, self._flat, self.world)
+                    allreduce_mean_(self.params, self._flat, self.world, timing=self.comm_events)
                 nn.utils.clip_grad_norm_(self.params, cfg.max_grad_norm)
                 self.opt.step()
                 with torch.no_grad():
@@ -399,6 +459,12 @@ class PPO:
         steps = epochs * nmb if max_minibatches is None else min(epochs * nmb, max_minibatches)
         mstats = torch.zeros(max(steps, 1), 4, dtype=torch.float32, device=self.device)
         perms, sums = {}, {}
+        # the full minibatches' advantage statistics of an epoch in one launch when that launch fits
+        # (grid y <= 65,535 minibatches, 4 KB of float64 sums each); a short last minibatch (SB3
+        # yields one when batch_size does not divide the buffer) and larger counts run grads' own
+        # statistics pre-pass -- the same sums either way
+        n_full = total // B
+        epoch_stats = 1 <= n_full <= EPOCH_STATS_MAX_MINIBATCHES
 
         def index_of(k):  # the k-th minibatch of the update: epoch k // nmb, slot k % nmb
             e, m = divmod(k, nmb)
@@ -406,15 +472,16 @@ class PPO:
                 perms[e] = epoch_permutation(total, self.device)
                 # every minibatch's advantage statistics of the epoch in one launch (the rollout
                 # buffer's advantages do not change during the update)
-                sums[e] = self._learner.adv_stats_epoch(adv, perms[e], B, nmb)
-            return perms[e][m * B:(m + 1) * B], (None if sums[e] is None else sums[e][m])
+                sums[e] = self._learner.adv_stats_epoch(adv, perms[e], B, n_full) if epoch_stats else None
+            row = sums[e][m] if sums[e] is not None and m < n_full else None
+            return perms[e][m * B:min(total, (m + 1) * B)], row
 
         done = 0
         for k in range(steps):
             idx, adv_sums = index_of(k)
             self._learner.grads(obs, act, logp_old, adv, ret, idx, mstats[k], adv_sums=adv_sums)
             if self.world > 1:
-                allreduce_mean_(self.params, self._flat, self.world)
+                allreduce_mean_(self.params, self._flat, self.world, timing=self.comm_events)
             self._adam.step()  # clip_grad_norm_ + Adam.step (quad_clip_adam)
             perms.pop(k // nmb - 1, None)
             sums.pop(k // nmb - 1, None)
