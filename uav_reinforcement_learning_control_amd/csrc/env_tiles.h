@@ -110,8 +110,8 @@ __device__ __forceinline__ void load_env(const KParams& p, int i, EnvRegs<float>
 }
 
 // the fields the physics and the observation need (not the voltage / CTBR integral: k_step_h's
-// helper waves own the control path)
-template <int AUX = 0>
+// helper waves own the control path; with STEP = false not the step counter either)
+template <int AUX = 0, bool STEP = true>
 __device__ __forceinline__ void load_env_motion(const KParams& p, int i, EnvRegs<float>& e) {
   const TilesA<AUX> S(p);
   const uint32_t o = env_off(uint32_t(i));
@@ -132,11 +132,21 @@ __device__ __forceinline__ void load_env_motion(const KParams& p, int i, EnvRegs
   e.step = int32_t(S.ldu(F_STEP, o));
 }
 
-template <int AUX = 0>
+// A per-lane offset made opaque in the block that uses it (fresh_off): the field offsets o + f * 256
+// are then formed in THIS basic block, where instruction selection folds them into the store's
+// immediate. Without it the compiler CSEs them with the load burst's (a different block), and
+// since selection folds addressing modes only within one block, each store took its own
+// materialized address: 15 v_add held across the step (15 VGPRs -- k_step_hd spilled) and 15 VALU.
+__device__ __forceinline__ uint32_t fresh_off(uint32_t o) {
+  asm volatile("" : "+v"(o));
+  return o;
+}
+
+template <int AUX = 0, bool STEP = true>
 __device__ __forceinline__ void store_env(const KParams& p, int i, const EnvRegs<float>& e,
                                           bool ctbr) {
   const TilesA<AUX> S(p);
-  const uint32_t o = env_off(uint32_t(i));
+  const uint32_t o = fresh_off(env_off(uint32_t(i)));
 #pragma unroll
   for (int j = 0; j < 3; j++) S.st(F_QPOS + j, o, e.pos[j]);
 #pragma unroll
@@ -156,7 +166,7 @@ __device__ __forceinline__ void store_env(const KParams& p, int i, const EnvRegs
 #pragma unroll
     for (int j = 0; j < 3; j++) S.st(F_RINT + j, o, e.rint[j]);
   }
-  S.stu(F_STEP, o, uint32_t(e.step));
+  if (STEP) S.stu(F_STEP, o, uint32_t(e.step));
 }
 
 // Mark a loaded value as consumed here, before the step's first store. gfx9's vmcnt retires
