@@ -381,6 +381,15 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       pfs[2] = g.ret[row];
     }
   };
+  // features 12..15 of every observation image row: 1.0 (dW1's column 12 is db1), 0, 0, 0 -- both
+  // buffers, once (the per-round staging writes features 0..11 only)
+  if (tid < 2 * RND) {
+    const bf16x4 one = {__bf16(1.f), __bf16(0.f), __bf16(0.f), __bf16(0.f)}, zero = {};
+    char* const XO = L + B_XO + (tid / RND) * 3 * XIMG + (tid % RND) * XROW + 24;
+    *reinterpret_cast<bf16x4*>(XO) = one;
+    *reinterpret_cast<bf16x4*>(XO + XIMG) = zero;
+    *reinterpret_cast<bf16x4*>(XO + 2 * XIMG) = zero;
+  }
   gather(index_of(0));
   int64_t next_row = index_of(1);
   __syncthreads();
@@ -405,18 +414,15 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     LP(0);
     char* const XO = L + B_XO + (rd & 1) * 3 * XIMG;
     float* const SCI = Lf + B_SC / 4 + (rd & 1) * RND * 8;
-    if (tid < 3 * RND) {
+    // threads 0..191 = waves 0-2, 192..255 = wave 3: a wave-uniform role (a scalar branch); the
+    // constant columns 12..15 are written once before the loop, so no lane branches here (the
+    // kernel's 8 spilled VGPRs went to 0)
+    if (__builtin_amdgcn_readfirstlane(tid) < 3 * RND) {
       const float v[4] = {pf.x, pf.y, pf.z, pf.w};
       const X3h x = split4(v);
       const int c = tid % 3;
 #pragma unroll
       for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(XO + p * XIMG + srow * XROW + 8 * c) = x.p[p];
-      if (c == 2) {  // features 12..15: 1.0 (dW1's column 12 is db1), 0, 0, 0
-        const bf16x4 one = {__bf16(1.f), __bf16(0.f), __bf16(0.f), __bf16(0.f)}, zero = {};
-        *reinterpret_cast<bf16x4*>(XO + srow * XROW + 24) = one;
-        *reinterpret_cast<bf16x4*>(XO + XIMG + srow * XROW + 24) = zero;
-        *reinterpret_cast<bf16x4*>(XO + 2 * XIMG + srow * XROW + 24) = zero;
-      }
     } else {
       *reinterpret_cast<float4*>(SCI + srow * 8) = pf;
       SCI[srow * 8 + 4] = pfs[0]; SCI[srow * 8 + 5] = pfs[1]; SCI[srow * 8 + 6] = pfs[2];

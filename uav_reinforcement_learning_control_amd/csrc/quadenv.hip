@@ -300,10 +300,7 @@ constexpr int H_SMALL = 32768;
 #define QD_H_PRE 1  // Philox blocks of the helper's reset draw issued before barrier (C): 1 measured best (below)
 #endif
 constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
-constexpr int HCTL = 9;   // words per env from the control helper: Fsum, taum 3, volt, flags, rint 3
-// CT word 5: helper -> step wave (barrier C) bit 0 = bad ctrl, bit 1 = the time limit is reached;
-// step wave -> helper (barrier 1) 1 = the env resets
-constexpr uint32_t CT_BADCTRL = 1u, CT_TRUNC = 2u;
+constexpr int HCTL = 9;   // floats per env from the control helper: Fsum, taum 3, volt, bad ctrl, rint 3
 template <int KIND, bool CTBR, int HB, bool NT>
 __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, const float4* __restrict__ act,
                                             QuadStepOut out, float4* lds, float* H, float* CT) {
@@ -336,11 +333,6 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     const float4 a4 = act[i];
     const float a[4] = {a4.x, a4.y, a4.z, a4.w};
     const float volt = S.ld(F_VOLT, vo);
-    // the step and episode counters are the helper's: it tells the step wave whether the time
-    // limit is reached (CT) and stores both counters once the step wave has said whether the env
-    // resets (after barrier 1) -- two values fewer held by the step wave from its load burst to
-    // its stores (k_step_hd spilled them under its 7-wave budget) and two loads off its burst
-    const uint32_t step1 = S.ldu(F_STEP, vo) + 1u;
     float w[3] = {0.f, 0.f, 0.f}, ri[3] = {0.f, 0.f, 0.f};
     if (CTBR) {
 #pragma unroll
@@ -354,8 +346,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #pragma unroll
     for (int j = 0; j < 3; j++) CT[(1 + j) * HB + l] = m.taum[j];
     CT[4 * HB + l] = c.volt;
-    CT[5 * HB + l] = __uint_as_float((any_bad_ctrl<float>(c.F) ? CT_BADCTRL : 0u) |
-                                     (int32_t(step1) >= K.max_steps ? CT_TRUNC : 0u));
+    CT[5 * HB + l] = any_bad_ctrl<float>(c.F) ? 1.f : 0.f;
     if (CTBR) {
 #pragma unroll
       for (int j = 0; j < 3; j++) CT[(6 + j) * HB + l] = ri[j];
@@ -403,21 +394,26 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #pragma unroll
     for (int f = 0; f < HROW; f++) H[f * HB + l] = row[f];
     QD_STAMP(stamps, 4);
-    __syncthreads();  // (1) the image is complete; the step wave's reset decisions are in CT
+    __syncthreads();  // (1) the image is complete
     QD_STAMP(stamps, 5);
-    if (live) {  // the counters: a reset starts the next episode at step 0
-      const bool rs = __float_as_uint(CT[5 * HB + l]) != 0u;
-      S.stu(F_STEP, fresh_off(vo), rs ? 0u : step1);
-      if (rs) S.stu(F_EP, vo, ep + 1u);
-    }
     __syncthreads();  // (2) the obs rows are staged
     QD_STAMP(stamps, 6);
   } else {  // ---- step
     float obs[12];
     EnvRegs<float> e;
-    load_env_motion<AUX, false>(p, i, e);
-    if (stamps) { QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.th, 4); QD_PIN_N(e.v, 3);
-                  QD_PIN_N(e.w, 3); QD_PIN_N(e.s, 4); QD_PIN_N(e.target, 3); }
+#if defined(QD_H_NOCTL)  // A/B builds only: the step wave runs the control path itself (round 2)
+    load_env<AUX>(p, i, e, CTBR);
+    const uint32_t ep = S.ldu(F_EP, vo);
+    const float4 a4 = act[i];
+    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+    StepRes r;
+    env_step<float, CTBR>(K, e, a, r);
+    __syncthreads();  // (C)
+#else
+    load_env_motion<AUX>(p, i, e);
+    const uint32_t ep = S.ldu(F_EP, vo);
+    if (stamps) { QD_PIN(ep); QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.th, 4); QD_PIN_N(e.v, 3);
+                  QD_PIN_N(e.w, 3); QD_PIN_N(e.s, 4); QD_PIN_N(e.target, 3); QD_PIN(e.step); }
     QD_STAMP(stamps, 1);
     // mujoco.mj_step up to the controls: mj_checkPos/Vel, gravity + base + prop drag
     const bool bad = check_state(e);
@@ -434,17 +430,13 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #pragma unroll
     for (int j = 0; j < 3; j++) m.taum[j] = CT[(1 + j) * HB + l];
     e.volt = CT[4 * HB + l];
-    const uint32_t flags = __float_as_uint(CT[5 * HB + l]);
-    // the step counter as env_post needs it for the truncation test (the helper stores it): the
-    // limit's predecessor when the limit is reached, else a count that stays below it
-    e.step = (flags & CT_TRUNC) ? K.max_steps - 1 : -1;
     if (CTBR) {
 #pragma unroll
       for (int j = 0; j < 3; j++) e.rint[j] = CT[(6 + j) * HB + l];
     } else {
       e.rint[0] = e.rint[1] = e.rint[2] = 0.f;
     }
-    if (bad || (flags & CT_BADCTRL)) {  // mj_fwdActuation: bad state / bad ctrl -> zero ctrl
+    if (bad || CT[5 * HB + l] != 0.f) {  // mj_fwdActuation: bad state / bad ctrl -> zero ctrl
       const double z[4] = {0.0, 0.0, 0.0, 0.0};
       m = wrench_of<float, true>(K.ph, z, true);
     }
@@ -453,26 +445,25 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     QD_STAMP(stamps, 4);
     StepRes r;
     env_post(K, e, r);
+#endif
     if (stamps) { QD_PIN_N(r.obs, 12); QD_PIN(r.reward); QD_PIN(uint32_t(r.term)); }
     QD_STAMP(stamps, 5);
+    settle(ep);
     const uint32_t o = uint32_t(i) * 4u;
     if (live) {
       sto(out.reward, o, r.reward);
       sto(out.terminated, uint32_t(i), uint8_t(r.term));
       sto(out.truncated, uint32_t(i), uint8_t(r.trunc));
       if (out.state12) store_row12(out.state12, uint32_t(i), r.state12);
-      if (out.target_info) {  // (info="full" only: both counters read here, before the helper's stores)
+      if (out.target_info) {
         float info[9];
-        EnvRegs<float> ec = e;
-        ec.step = int32_t(S.ldu(F_STEP, vo)) + 1;
-        target_info_of<KIND>(K, p, i, ec, S.ldu(F_EP, vo), info);
+        target_info_of<KIND>(K, p, i, e, ep, info);
         store_target_info(out.target_info, i, info);
       }
     }
 #pragma unroll
     for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
     const bool rs = live && (r.term || r.trunc) && p.auto_reset;
-    CT[5 * HB + l] = __uint_as_float(rs ? 1u : 0u);  // for the helper's counter stores
     QD_STAMP(stamps, 6);
     __syncthreads();  // (1)
     QD_STAMP(stamps, 7);
@@ -491,8 +482,10 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #pragma unroll
       for (int j = 0; j < 12; j++) obs[j] = row[16 + j];
       e.volt = float(K.vnom);
+      e.step = 0;
+      S.stu(F_EP, fresh_off(vo), ep + 1u);
     }
-    if (live) store_env<AUX, false>(p, i, e, CTBR);  // (the counters: the helper)
+    if (live) store_env<AUX>(p, i, e, CTBR);
     lds[3 * l + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
     lds[3 * l + 1] = make_float4(obs[4], obs[5], obs[6], obs[7]);
     lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
@@ -536,8 +529,9 @@ __global__ __launch_bounds__(2 * HB) void k_step_h(float* tiles, const float4* _
 }
 
 // k_step_hd: k_step_h's DRAM form (64-env blocks, nt state) with a floor of 7 waves per SIMD on its
-// register budget (72 VGPRs instead of 74-76 and 6 waves; round 4: 5 of them spilled, none since the
-// store offsets are block-local (fresh_off) and the counters live on the helper waves). More waves keep more
+// register budget (72 VGPRs, 5 of them spilled, instead of 74-76 and 6 waves). (Round 5: moving the
+// step / episode counters to the helper waves removed the spills but cost 13 us at 4M envs -- the
+// counters' stores left the step wave's store burst; profiles/r05/step_counters_ab.txt.) More waves keep more
 // state bytes in flight where the batch streams from DRAM: 4M envs 250.0-251.6 vs 264.9-265.8 us,
 // 8M 511.7-513.0 vs 546.5-547.9; where the Infinity Cache still serves part of it the spills cost
 // more than the waves buy (2M 108 vs 95, 3M 161 vs 145; profiles/r04/r4_step_hw7_ab.txt). Same body,
@@ -1654,8 +1648,8 @@ bool h_wide(const QuadHandle* h, int64_t count) {
 
 // k_step_hd instead of k_step_h<.., 64, true> for a launch of `count` envs: from 4M envs, where the
 // step streams from DRAM (the comment at k_step_hd). QUADENV_HD=0 / 1 pins it (A/B and tests).
-// Only HoverEnv without the rate controller by size: its step fits the 7-wave budget (72 VGPRs,
-// no spills); the trajectory and CTBR kinds spill 15-130 VGPRs there and keep k_step_h.
+// Only HoverEnv without the rate controller by size: the trajectory and CTBR kinds spill 15-130
+// VGPRs under its 7-wave budget (HoverEnv: 5) and keep k_step_h.
 bool hd_form(const QuadHandle* h, int64_t count) {
   if (h_wide(h, count) || !nt_state(h, count)) return false;
   if (h->hd >= 0) return h->hd != 0;
