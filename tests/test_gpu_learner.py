@@ -94,16 +94,19 @@ def _torch_grads(pol, dtype, obs, act, logp_old, adv, ret, idx, cfg):
     return [p.grad.double() for p in _ordered(ref)], torch.stack([pg, vf, ent, cf]).detach().double()
 
 
+LEARNER_FORMS = {"x3": 1, "f32": 0}
+
+
 @pytest.fixture(params=["x3", "f32"])
 def learner_form(request, monkeypatch):
     """Both forms of quad_ppo_grad: k_ppo_grad_x3 (bf16 MFMA on three-piece splits, the default)
     and k_ppo_grad (f32-input MFMA), selected per call by QUADENV_LEARNER."""
     from uav_reinforcement_learning_control_amd import _native as N
-    if request.param == "f32":
-        monkeypatch.setenv("QUADENV_LEARNER", "f32")
-    else:
+    if request.param == "x3":
         monkeypatch.delenv("QUADENV_LEARNER", raising=False)
-    assert N.lib().quad_ppo_grad_form() == (1 if request.param == "x3" else 0)
+    else:
+        monkeypatch.setenv("QUADENV_LEARNER", request.param)
+    assert N.lib().quad_ppo_grad_form() == LEARNER_FORMS[request.param]
     return request.param
 
 
