@@ -98,6 +98,12 @@ __global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, c
 
 
 
+// tile 1's dh2 in dW2's first k-steps (see the dh2 phase; round 5: 741-743 vs 755-759 us per
+// 524,288-row minibatch same-box, the same gradient bits; 0 = dh2 of both tiles, then B4, then dW2)
+#ifndef QD_X3_DH2OV
+#define QD_X3_DH2OV 1
+#endif
+
 // QD_LPROBE (tools/probe/probe_learner.py builds only, never the product): the dump build records
 // per-wave s_memtime stamps at the phase boundaries of round 2 into g.dump instead of the hidden
 // pre-activations (sched barriers around each stamp: the probe build is slower; use the shares)
@@ -432,34 +438,47 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     }
     LP(7);
     // ---- dh2 (E form) -> DH2 pieces; dW3 per lane
+    // (one 4-neuron chunk of tile t: dh2 = relu'(h2) (d W3), dW3 / db2 per lane, the DH2 pieces)
+    auto dh2_chunk = [&](int t, int gg) {
+      float v[4];
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
+      for (int u = 0; u < 4; u++) {
+        const int r = 4 * gg + u;
+        const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * (32 * w + acc_row(r, h)));
+        const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
+        float gsum = 0.f;
 #pragma unroll
-      for (int gg = 0; gg < 4; gg++) {
-        float v[4];
+        for (int k = 0; k < NOUT; k++) gsum = fmaf(wk[k], d[t][k], gsum);
+        v[u] = h2[t][r] > 0.f ? gsum : 0.f;
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int r = 4 * gg + u;
-          const float4 w3 = *reinterpret_cast<const float4*>(Lf + B_W3T / 4 + 4 * (32 * w + acc_row(r, h)));
-          const float wk[4] = {w3.x, w3.y, w3.z, w3.w};
-          float gsum = 0.f;
-#pragma unroll
-          for (int k = 0; k < NOUT; k++) gsum = fmaf(wk[k], d[t][k], gsum);
-          v[u] = h2[t][r] > 0.f ? gsum : 0.f;
-#pragma unroll
-          for (int k = 0; k < NOUT; k++) dW3[k][r] = fmaf(d[t][k], h2[t][r], dW3[k][r]);  // h2: relu'd
-          dB2[r] += v[u];
-        }
-        const X3h x = split4(v);
-        const int off = soff(32 * t + l32, 4 * w + gg) + 8 * h;
-#pragma unroll
-        for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_DH2P + p * IMG + off) = x.p[p];
+        for (int k = 0; k < NOUT; k++) dW3[k][r] = fmaf(d[t][k], h2[t][r], dW3[k][r]);  // h2: relu'd
+        dB2[r] += v[u];
       }
-    }
+      const X3h x = split4(v);
+      const int off = soff(32 * t + l32, 4 * w + gg) + 8 * h;
+#pragma unroll
+      for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_DH2P + p * IMG + off) = x.p[p];
+    };
+#if QD_X3_DH2OV
+    // dW2 reads only this wave's own DH2 columns (its neurons) and the H1 image (complete since
+    // B2), so it needs no barrier: tile 0's dh2 first, then dW2's first two k-steps (rows 0..31 =
+    // tile 0) with tile 1's dh2 chunks in their issue gaps, written before the k-step-2 reads of
+    // rows 32..47 are issued (program order within the wave); B4 (every wave's DH2 columns) then
+    // guards dh1's row reads. Per register r the dW3 / db2 sums keep the order tile 0, tile 1.
+#pragma unroll
+    for (int gg = 0; gg < 4; gg++) dh2_chunk(0, gg);
+    LP(8);
+    LP(9);
+#else
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int gg = 0; gg < 4; gg++) dh2_chunk(t, gg);
     LP(8);
     X3_BAR();  // B4: DH2 image complete
     const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);  // dh1's first two k-steps: in flight through dW2
     LP(9);
+#endif
 
 #if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
@@ -487,6 +506,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
           if (jb < 3) bn = trblk(B_H1P, s, 4 * (jb + 1) + tr_col);
           else if (s < 3) { an = trblk(B_DH2P, s + 1, 4 * w + tr_col); bn = trblk(B_H1P, s + 1, tr_col); }
           dW2[jb] = mma3(a, b, dW2[jb]);
+#if QD_X3_DH2OV
+          if (s < 2 && (jb & 1) == 0) dh2_chunk(1, 2 * s + (jb >> 1));  // before (s = 1, jb = 3)'s k-step-2 reads
+#endif
           if (jb < 3) X3_PIPE(6, 6);
           else if (s < 3) X3_PIPE(12, 6);
           X3_SB();
@@ -495,6 +517,10 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         }
       }
     }
+#endif
+#if QD_X3_DH2OV
+    X3_BAR();  // B4: every wave's DH2 columns (dh1 reads whole rows)
+    const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);
 #endif
     LP(10);
 #if !defined(QD_X3_NODH1)
