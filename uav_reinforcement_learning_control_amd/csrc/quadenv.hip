@@ -299,6 +299,13 @@ constexpr int H_SMALL = 32768;
 #ifndef QD_H_PRE
 #define QD_H_PRE 1  // Philox blocks of the helper's reset draw issued before barrier (C): 1 measured best (below)
 #endif
+// Small batches (64-env blocks, default cache policy: up to H_SMALL envs): each step lane stores its
+// own obs row (three 16-byte stores; the non-resetting lanes before barrier 1, under the helper's
+// reset draw) instead of the block's LDS transpose + barrier 2 + the shared copy -- 3.38 vs 3.45-3.46
+// us at 4,096 envs; at 65,536 (256-env blocks) 6.43-6.54 vs 5.60-5.77, at 1M 54.5 vs 52.2-52.3, at 4M
+// (k_step_hd) 262 vs 248-249, so those keep the transpose (profiles/r05/step_obs_direct_ab.txt)
+template <int HB, bool NT>
+constexpr bool obs_direct() { return HB == 64 && !NT; }
 constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
 constexpr int HCTL = 9;   // floats per env from the control helper: Fsum, taum 3, volt, bad ctrl, rint 3
 template <int KIND, bool CTBR, int HB, bool NT>
@@ -396,7 +403,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     QD_STAMP(stamps, 4);
     __syncthreads();  // (1) the image is complete
     QD_STAMP(stamps, 5);
-    __syncthreads();  // (2) the obs rows are staged
+    if constexpr (!obs_direct<HB, NT>()) __syncthreads();  // (2) the obs rows are staged
     QD_STAMP(stamps, 6);
   } else {  // ---- step
     float obs[12];
@@ -465,6 +472,9 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
     const bool rs = live && (r.term || r.trunc) && p.auto_reset;
     QD_STAMP(stamps, 6);
+    if constexpr (obs_direct<HB, NT>()) {
+      if (live && !rs) store_row12(out.obs, uint32_t(i), r.obs);  // before (1): under the helper's draw
+    }
     __syncthreads();  // (1)
     QD_STAMP(stamps, 7);
     if (rs) {
@@ -484,19 +494,24 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
       e.volt = float(K.vnom);
       e.step = 0;
       S.stu(F_EP, fresh_off(vo), ep + 1u);
+      if constexpr (obs_direct<HB, NT>()) store_row12(out.obs, uint32_t(i), obs);
     }
     if (live) store_env<AUX>(p, i, e, CTBR);
-    lds[3 * l + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
-    lds[3 * l + 1] = make_float4(obs[4], obs[5], obs[6], obs[7]);
-    lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
+    if constexpr (!obs_direct<HB, NT>()) {
+      lds[3 * l + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
+      lds[3 * l + 1] = make_float4(obs[4], obs[5], obs[6], obs[7]);
+      lds[3 * l + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
+    }
     QD_STAMP(stamps, 8);
-    __syncthreads();  // (2)
+    if constexpr (!obs_direct<HB, NT>()) __syncthreads();  // (2)
     QD_STAMP(stamps, 9);
   }
-  // the block's [HB,12] obs rows as contiguous float4 stores, shared by all 2 x HB threads
-  const int nf4 = min(HB, end - block_first) * 3;
-  float4* dst = reinterpret_cast<float4*>(out.obs + size_t(block_first) * 12);
-  for (int idx = tid; idx < nf4; idx += 2 * HB) dst[idx] = lds[idx];
+  if constexpr (!obs_direct<HB, NT>()) {
+    // the block's [HB,12] obs rows as contiguous float4 stores, shared by all 2 x HB threads
+    const int nf4 = min(HB, end - block_first) * 3;
+    float4* dst = reinterpret_cast<float4*>(out.obs + size_t(block_first) * 12);
+    for (int idx = tid; idx < nf4; idx += 2 * HB) dst[idx] = lds[idx];
+  }
 #if defined(QD_PROBE)
   QD_STAMP(stamps, 10);
   if (stamps && (tid & 63) == 0) {  // wave (block, w): 16 words
