@@ -96,35 +96,6 @@ __device__ __forceinline__ void reset_words_shfl(const KParams& p, uint32_t (&re
   __builtin_amdgcn_wave_barrier();
 }
 
-// QD_ROLL_OBSLDS: the buffer's observation rows (48 B per env) go out as contiguous float4 stores
-// through a per-wave LDS stage, one half-wave (32 rows, 1.5 KB) at a time, instead of three 16-byte
-// stores per lane at a 48-byte stride (NT = 2 only; the nets leave ~9 KB of the LDS)
-#ifndef QD_ROLL_OBSLDS
-#define QD_ROLL_OBSLDS 0
-#endif
-__device__ __forceinline__ void store_rows_staged(float4* __restrict__ st, float* __restrict__ base, size_t row0,
-                                                  int n_valid, const float v[12]) {
-  const int lane = __lane_id();
-#pragma unroll
-  for (int half = 0; half < 2; half++) {
-    if ((lane >> 5) == half) {
-#pragma unroll
-      for (int k = 0; k < 3; k++) st[3 * (lane & 31) + k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int nv = min(max(n_valid - 32 * half, 0), 32) * 3;  // float4s of this half's valid rows
-    float4* dst = reinterpret_cast<float4*>(base + (row0 + 32 * half) * 12);
-    const float4 a = st[lane], b = st[64 + (lane & 31)];
-    if (lane < nv) dst[lane] = a;
-    if (lane < 32 && 64 + lane < nv) dst[64 + lane] = b;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-}
-
 __device__ __forceinline__ void store_row(float* __restrict__ base, size_t row, const float v[12]) {
   float4* b4 = reinterpret_cast<float4*>(base + row * 12);
   b4[0] = make_float4(v[0], v[1], v[2], v[3]);
@@ -168,9 +139,6 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
   constexpr int BLK = 512 / NT, WAVES = BLK / 64;
   extern __shared__ float lds[];
   __shared__ uint32_t renv[WAVES][64], rep[WAVES][64];
-#if QD_ROLL_OBSLDS
-  __shared__ float4 obs_stage[NT == 2 ? WAVES : 1][96];
-#endif
   const int w = threadIdx.x >> 6;
   const bool h = (threadIdx.x & 32) != 0;
   const int i_raw = blockIdx.x * RBLOCK + (NT == 2 ? int(threadIdx.x) : w * 32 + int(threadIdx.x & 31));
@@ -230,14 +198,9 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
 #endif
     float act[ACT], ac[ACT], lp = 0.f;
     sample_action<NT>(a, p, i, t, h, mean, sd, lstd, act, ac, lp);
-#if QD_ROLL_OBSLDS
-    if constexpr (NT == 2)  // every lane takes part (the valid-row count bounds the stores)
-      store_rows_staged(obs_stage[w], a.obs_copy, size_t(t % a.rows) * n + size_t(blockIdx.x * RBLOCK + 64 * w),
-                        p.n - (int(blockIdx.x) * RBLOCK + 64 * w), ob);
-#endif
     if (owner) {
 #if !defined(QD_ROLL_NOOBSCOPY)  // cost ablation (tools/rollout_variants.sh only): the strided obs rows
-      if (!QD_ROLL_OBSLDS || NT != 2) store_row(a.obs_copy, row, ob);
+      store_row(a.obs_copy, row, ob);
 #endif
       reinterpret_cast<float4*>(a.actions)[row] = make_float4(act[0], act[1], act[2], act[3]);
       a.log_prob[row] = lp;
