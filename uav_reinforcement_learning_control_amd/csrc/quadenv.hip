@@ -306,6 +306,20 @@ constexpr int H_SMALL = 32768;
 // (k_step_hd) 262 vs 248-249, so those keep the transpose (profiles/r05/step_obs_direct_ab.txt)
 template <int HB, bool NT>
 constexpr bool obs_direct() { return HB == 64 && !NT; }
+// Without CTBR, the helper image H and the control block CT as env-major 16-byte rows: the helper
+// writes an env's 28 image words as seven 16-byte stores (and its control words as two) and a
+// resetting step lane reads its row back the same way, instead of one word per field; same bits,
+// 4,096 envs 3.32 vs 3.36 us, 4M 249.8-250.6 vs 253.8-254.6, 65,536 and 1M unchanged
+// (profiles/r05/step_rowmajor_image_ab.txt). QD_H_ROWMAJOR=0: the field-major layout (A/B builds)
+#ifndef QD_H_ROWMAJOR
+#define QD_H_ROWMAJOR 1
+#endif
+// H / CT layout: field-major [f][HB], or (QD_H_ROWMAJOR, no CTBR) 16-byte env rows (H: 28 words, CT:
+// CT_STRIDE); the CTBR kinds keep the field-major forms (config 5 at 65,536 envs measured 5.92 vs
+// 5.78 us with row-major H)
+template <bool CTBR>
+constexpr bool ct_rows() { return QD_H_ROWMAJOR && !CTBR; }
+constexpr int CT_STRIDE = 8;  // words per env row of CT (6 used)
 constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
 constexpr int HCTL = 9;   // floats per env from the control helper: Fsum, taum 3, volt, bad ctrl, rint 3
 template <int KIND, bool CTBR, int HB, bool NT>
@@ -349,11 +363,17 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     QD_STAMP(stamps, 1);
     const Ctl<float> c = env_control<float, CTBR>(K, volt, w, ri, a);
     const Wrench<float> m = wrench_of<float, true>(K.ph, c.F, false);  // F = clip(., 0, max) * vs >= 0
-    CT[0 * HB + l] = m.Fsum;
+    if constexpr (ct_rows<CTBR>()) {
+      reinterpret_cast<float4*>(CT)[l * (CT_STRIDE / 4)] = make_float4(m.Fsum, m.taum[0], m.taum[1], m.taum[2]);
+      reinterpret_cast<float4*>(CT)[l * (CT_STRIDE / 4) + 1] =
+          make_float4(c.volt, any_bad_ctrl<float>(c.F) ? 1.f : 0.f, 0.f, 0.f);
+    } else {
+      CT[0 * HB + l] = m.Fsum;
 #pragma unroll
-    for (int j = 0; j < 3; j++) CT[(1 + j) * HB + l] = m.taum[j];
-    CT[4 * HB + l] = c.volt;
-    CT[5 * HB + l] = any_bad_ctrl<float>(c.F) ? 1.f : 0.f;
+      for (int j = 0; j < 3; j++) CT[(1 + j) * HB + l] = m.taum[j];
+      CT[4 * HB + l] = c.volt;
+      CT[5 * HB + l] = any_bad_ctrl<float>(c.F) ? 1.f : 0.f;
+    }
     if (CTBR) {
 #pragma unroll
       for (int j = 0; j < 3; j++) CT[(6 + j) * HB + l] = ri[j];
@@ -398,8 +418,14 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
                              e.target[0], e.target[1], e.target[2],
                              obs[0], obs[1], obs[2], obs[3], obs[4], obs[5], obs[6], obs[7], obs[8], obs[9],
                              obs[10], obs[11]};
+    if constexpr (ct_rows<CTBR>()) {  // env-major rows (112 B, 16-byte aligned): seven 16-byte writes
 #pragma unroll
-    for (int f = 0; f < HROW; f++) H[f * HB + l] = row[f];
+      for (int q = 0; q < HROW / 4; q++)
+        reinterpret_cast<float4*>(H)[l * (HROW / 4) + q] = make_float4(row[4 * q], row[4 * q + 1], row[4 * q + 2], row[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int f = 0; f < HROW; f++) H[f * HB + l] = row[f];
+    }
     QD_STAMP(stamps, 4);
     __syncthreads();  // (1) the image is complete
     QD_STAMP(stamps, 5);
@@ -433,17 +459,27 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     __syncthreads();  // (C)
     QD_STAMP(stamps, 3);
     Wrench<float> m;
-    m.Fsum = CT[0 * HB + l];
+    float ct_bad;
+    if constexpr (ct_rows<CTBR>()) {
+      const float4 c0 = reinterpret_cast<const float4*>(CT)[l * (CT_STRIDE / 4)];
+      const float4 c1 = reinterpret_cast<const float4*>(CT)[l * (CT_STRIDE / 4) + 1];
+      m.Fsum = c0.x; m.taum[0] = c0.y; m.taum[1] = c0.z; m.taum[2] = c0.w;
+      e.volt = c1.x;
+      ct_bad = c1.y;
+    } else {
+      m.Fsum = CT[0 * HB + l];
 #pragma unroll
-    for (int j = 0; j < 3; j++) m.taum[j] = CT[(1 + j) * HB + l];
-    e.volt = CT[4 * HB + l];
+      for (int j = 0; j < 3; j++) m.taum[j] = CT[(1 + j) * HB + l];
+      e.volt = CT[4 * HB + l];
+      ct_bad = CT[5 * HB + l];
+    }
     if (CTBR) {
 #pragma unroll
       for (int j = 0; j < 3; j++) e.rint[j] = CT[(6 + j) * HB + l];
     } else {
       e.rint[0] = e.rint[1] = e.rint[2] = 0.f;
     }
-    if (bad || CT[5 * HB + l] != 0.f) {  // mj_fwdActuation: bad state / bad ctrl -> zero ctrl
+    if (bad || ct_bad != 0.f) {  // mj_fwdActuation: bad state / bad ctrl -> zero ctrl
       const double z[4] = {0.0, 0.0, 0.0, 0.0};
       m = wrench_of<float, true>(K.ph, z, true);
     }
@@ -480,8 +516,16 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     if (rs) {
       if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
       float row[HROW];
+      if constexpr (ct_rows<CTBR>()) {
 #pragma unroll
-      for (int f = 0; f < HROW; f++) row[f] = H[f * HB + l];
+        for (int q = 0; q < HROW / 4; q++) {
+          const float4 v = reinterpret_cast<const float4*>(H)[l * (HROW / 4) + q];
+          row[4 * q] = v.x; row[4 * q + 1] = v.y; row[4 * q + 2] = v.z; row[4 * q + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int f = 0; f < HROW; f++) row[f] = H[f * HB + l];
+      }
 #pragma unroll
       for (int j = 0; j < 3; j++) {
         e.pos[j] = row[j]; e.v[j] = row[7 + j]; e.w[j] = row[10 + j]; e.target[j] = row[13 + j];
@@ -533,8 +577,8 @@ __global__ __launch_bounds__(2 * HB) void k_step_h(float* tiles, const float4* _
   p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
   p.kc = kc;
   __shared__ float4 lds[HB * 3];
-  __shared__ float H[HROW * HB];
-  __shared__ float CT[(CTBR ? HCTL : HCTL - 3) * HB];
+  __shared__ __attribute__((aligned(16))) float H[HROW * HB];
+  __shared__ __attribute__((aligned(16))) float CT[(ct_rows<CTBR>() ? CT_STRIDE : (CTBR ? HCTL : HCTL - 3)) * HB];
   if constexpr (SPEC) {
     constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
     step_h_body<KIND, CTBR, HB, NT>(K, p, act, out, lds, H, CT);
@@ -558,8 +602,8 @@ void k_step_hd(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes
   p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
   p.kc = kc;
   __shared__ float4 lds[64 * 3];
-  __shared__ float H[HROW * 64];
-  __shared__ float CT[(CTBR ? HCTL : HCTL - 3) * 64];
+  __shared__ __attribute__((aligned(16))) float H[HROW * 64];
+  __shared__ __attribute__((aligned(16))) float CT[(ct_rows<CTBR>() ? CT_STRIDE : (CTBR ? HCTL : HCTL - 3)) * 64];
   if constexpr (SPEC) {
     constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
     step_h_body<KIND, CTBR, 64, true>(K, p, act, out, lds, H, CT);
