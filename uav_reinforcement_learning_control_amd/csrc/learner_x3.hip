@@ -104,6 +104,12 @@ __global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, c
 #define QD_X3_DH2OV 1
 #endif
 
+// the loss terms one row per lane (each row once per wave instead of once per lane half), both
+// tiles' dL/d(head) by lane-half swaps; 0 = two rows per lane (every row on both halves)
+#ifndef QD_X3_LOSS1
+#define QD_X3_LOSS1 1
+#endif
+
 // QD_LPROBE (tools/probe/probe_learner.py builds only, never the product): the dump build records
 // per-wave s_memtime stamps at the phase boundaries of round 2 into g.dump instead of the hidden
 // pre-activations (sched barriers around each stamp: the probe build is slower; use the shares)
@@ -198,7 +204,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   for (int k = 0; k < NOUT; k++) db3[k] = 0.f;
 #pragma unroll
   for (int k = 0; k < ACT; k++) dls[k] = 0.f;
-  const bool acc_lane = w == 0 && h == 0;  // one lane per row accumulates the per-row sums
+  [[maybe_unused]] const bool acc_lane = w == 0 && h == 0;  // QD_X3_LOSS1 0: one lane per row accumulates the per-row sums
 
   const int per_block = NOUT == ACT ? g.per_block : g.per_block_c;
   const int s0 = blk * per_block;
@@ -394,9 +400,22 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 
     // ---- per-row loss terms and dL/d(head output) (every wave, identical arithmetic)
     float d[2][NOUT];
+#if QD_X3_LOSS1
+    // one row per lane (row = lane: tile h, row l32), then both tiles' d on every lane by one
+    // v_permlane32_swap per output; the per-row sums accumulate on every lane of wave 0
+    {
+      const int e = lane;
+      const bool vrow = h ? valid[1] : valid[0];
+      const bool acc = w == 0 && vrow;
+      float dd[NOUT];
+#else
 #pragma unroll
     for (int t = 0; t < 2; t++) {
       const int e = 32 * t + l32;
+      const bool vrow = valid[t];
+      const bool acc = acc_lane && vrow;
+      float (&dd)[NOUT] = d[t];
+#endif
       const float* PT = Lf + B_PART / 4;
       float out[NOUT];
 #pragma unroll
@@ -419,22 +438,31 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         const float sa = A * r, sb = A * cr;
         const float w1 = sa < sb ? 1.f : (sa == sb ? 0.5f : 0.f);
         const float inr = (r >= 1.f - g.clip && r <= 1.f + g.clip) ? 1.f : 0.f;
-        const float dlp = valid[t] ? -g.inv_batch * A * (w1 + (1.f - w1) * inr) * r : 0.f;
+        const float dlp = vrow ? -g.inv_batch * A * (w1 + (1.f - w1) * inr) * r : 0.f;
 #pragma unroll
-        for (int k = 0; k < ACT; k++) d[t][k] = dlp * z[k] * isd[k];
+        for (int k = 0; k < ACT; k++) dd[k] = dlp * z[k] * isd[k];
         // the row sums as selects, not branches (the same operations on the accumulating lanes)
-        const bool acc = acc_lane && valid[t];
         st[0] = acc ? st[0] + -fminf(sa, sb) : st[0];
         st[2] = acc ? st[2] + (fabsf(r - 1.f) > g.clip ? 1.f : 0.f) : st[2];
 #pragma unroll
         for (int k = 0; k < ACT; k++) dls[k] = acc ? dls[k] + dlp * (z[k] * z[k] - 1.f) : dls[k];
       } else {
         const float diff = out[0] - SCI[e * 8 + 6];
-        d[t][0] = valid[t] ? 2.f * g.vf_coef * g.inv_batch * diff : 0.f;
-        st[1] = acc_lane && valid[t] ? st[1] + diff * diff : st[1];
+        dd[0] = vrow ? 2.f * g.vf_coef * g.inv_batch * diff : 0.f;
+        st[1] = acc ? st[1] + diff * diff : st[1];
       }
+#if QD_X3_LOSS1
 #pragma unroll
-      for (int k = 0; k < NOUT; k++) db3[k] = acc_lane ? db3[k] + d[t][k] : db3[k];
+      for (int k = 0; k < NOUT; k++) {
+        db3[k] = w == 0 ? db3[k] + dd[k] : db3[k];
+        const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(dd[k]), __float_as_uint(dd[k]), false, false);
+        d[0][k] = __uint_as_float(p[0]);  // lanes 0-31's value (tile 0's row) in every lane
+        d[1][k] = __uint_as_float(p[1]);  // lanes 32-63's (tile 1's)
+      }
+#else
+#pragma unroll
+      for (int k = 0; k < NOUT; k++) db3[k] = acc_lane ? db3[k] + dd[k] : db3[k];
+#endif
     }
     LP(7);
     // ---- dh2 (E form) -> DH2 pieces; dW3 per lane
@@ -642,7 +670,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o);
     if (l32 == 0) P[P_B2 + 32 * w + acc_row(r, h)] = x;
   }
-  if (w == 0) {  // lanes 0..31 hold the per-row sums (lanes 32..63 hold zeros)
+  if (w == 0) {  // the per-row sums (QD_X3_LOSS1: on every lane; else lanes 0..31, zeros above)
     float v[NOUT + ACT + 3];
     int nv = 0;
 #pragma unroll

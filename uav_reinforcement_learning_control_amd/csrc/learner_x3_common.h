@@ -170,8 +170,8 @@ __device__ __forceinline__ s16x4 rdtr(const char* L, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(L + off));
 }
 
-// x(lane) + x(lane ^ 32) in every lane, in the order lower half + upper half (v_permlane32_swap:
-// lanes 0-31 of the first result take lanes 32-63 of the source, lanes 32-63 of the second take 0-31)
+// x(lane) + x(lane ^ 32) in every lane (v_permlane32_swap of x with itself: the first result holds
+// lanes 0-31's values in every lane, the second lanes 32-63's; the sum is the same either order)
 __device__ __forceinline__ float xhalf_sum(float x) {
   const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(p[1]) + __uint_as_float(p[0]);
