@@ -110,6 +110,14 @@ __global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, c
 #define QD_X3_LOSS1 1
 #endif
 
+// how many k-steps ahead L2 / dh1 load their pre-split W2 pieces (global loads, L2-resident); round 5
+// A/B (profiles/r05/learner_wpf_ab.txt): 3 is 5 % slower (register pressure), 1 the same as 2
+#ifndef QD_X3_WPF
+#define QD_X3_WPF 2
+#endif
+constexpr int WPF = QD_X3_WPF, WRING = WPF + 1;
+static_assert(WPF >= 1 && WPF <= 3, "prefetch distance");
+
 // QD_LPROBE (tools/probe/probe_learner.py builds only, never the product): the dump build records
 // per-wave s_memtime stamps at the phase boundaries of round 2 into g.dump instead of the hidden
 // pre-activations (sched barriers around each stamp: the probe build is slower; use the shares)
@@ -262,7 +270,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       return x;
     };
 #define WLOAD(u, s) ldw(u, s)
-    const X3 wa0 = WLOAD(0, 0), wa1 = WLOAD(0, 1);  // L2's first two k-steps: in flight through L1
+    X3 wr[WRING];  // L2's first WPF k-steps: in flight through L1
+#pragma unroll
+    for (int k = 0; k < WPF; k++) wr[k] = WLOAD(0, k);
     LP(0);
     char* const XO = L + B_XO + (rd & 1) * 3 * XIMG;
     float* const SCI = Lf + B_SC / 4 + (rd & 1) * RND * 8;
@@ -328,15 +338,15 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
     for (int r = 0; r < 16; r++) { h2s[0][r] = 0.f; h2s[1][r] = 0.f; }
     {  // software pipeline: step s's MFMAs with step s + 1's reads and step s + 2's weight pieces in flight
-      X3 a = wa0, an = wa1, b[2];
+      X3 b[2];
 #pragma unroll
       for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int p = 0; p < 3; p++) b[t].p[p] = rd16(L, B_H1P + p * IMG + soff(32 * t + l32, 8 * h));
 #pragma unroll
       for (int s = 0; s < 8; s++) {
-        X3 ann, bn[2];
-        if (s < 6) ann = WLOAD(0, s + 2);
+        X3 bn[2];
+        if (s + WPF < 8) wr[(s + WPF) % WRING] = WLOAD(0, s + WPF);
         if (s < 7) {
 #pragma unroll
           for (int t = 0; t < 2; t++)
@@ -344,11 +354,11 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
             for (int p = 0; p < 3; p++) bn[t].p[p] = rd16(L, B_H1P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
         }
 #pragma unroll
-        for (int t = 0; t < 2; t++) mma3s(a, b[t], h2[t], h2s[t]);
-        if (s < 6) X3_PIPE_V(3, 6, 12);
+        for (int t = 0; t < 2; t++) mma3s(wr[s % WRING], b[t], h2[t], h2s[t]);
+        if (s + WPF < 8) X3_PIPE_V(3, 6, 12);
         else if (s < 7) X3_PIPE(6, 12);
         X3_SB();
-        if (s < 7) { a = an; an = ann; b[0] = bn[0]; b[1] = bn[1]; }
+        if (s < 7) { b[0] = bn[0]; b[1] = bn[1]; }
       }
     }
 #pragma unroll
@@ -504,7 +514,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       for (int gg = 0; gg < 4; gg++) dh2_chunk(t, gg);
     LP(8);
     X3_BAR();  // B4: DH2 image complete
-    const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);  // dh1's first two k-steps: in flight through dW2
+    X3 wr1[WRING];  // dh1's first WPF k-steps: in flight through dW2
+#pragma unroll
+    for (int k = 0; k < WPF; k++) wr1[k] = WLOAD(1, k);
     LP(9);
 #endif
 
@@ -548,7 +560,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #endif
 #if QD_X3_DH2OV
     X3_BAR();  // B4: every wave's DH2 columns (dh1 reads whole rows)
-    const X3 wb0 = WLOAD(1, 0), wb1 = WLOAD(1, 1);
+    X3 wr1[WRING];
+#pragma unroll
+    for (int k = 0; k < WPF; k++) wr1[k] = WLOAD(1, k);
 #endif
     LP(10);
 #if !defined(QD_X3_NODH1)
@@ -558,15 +572,15 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     for (int r = 0; r < 16; r++) { dh1[0][r] = 0.f; dh1[1][r] = 0.f; }
     f32x16 dh1s[2] = {dh1[0], dh1[1]};
     {  // software pipeline as L2: A = DH2 row reads, B = pre-split W2 columns
-      X3 b = wb0, bn = wb1, a[2];
+      X3 a[2];
 #pragma unroll
       for (int t = 0; t < 2; t++)
 #pragma unroll
         for (int p = 0; p < 3; p++) a[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, 8 * h));
 #pragma unroll
       for (int s = 0; s < 8; s++) {
-        X3 bnn, an[2];
-        if (s < 6) bnn = WLOAD(1, s + 2);
+        X3 an[2];
+        if (s + WPF < 8) wr1[(s + WPF) % WRING] = WLOAD(1, s + WPF);
         if (s < 7) {
 #pragma unroll
           for (int t = 0; t < 2; t++)
@@ -576,15 +590,15 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
         for (int t = 0; t < 2; t++) {
 #if defined(QD_X3_DH1ONE)
-          dh1[t] = mma3(a[t], b, dh1[t]);
+          dh1[t] = mma3(a[t], wr1[s % WRING], dh1[t]);
 #else
-          mma3s(a[t], b, dh1[t], dh1s[t]);
+          mma3s(a[t], wr1[s % WRING], dh1[t], dh1s[t]);
 #endif
         }
-        if (s < 6) X3_PIPE_V(3, 6, 12);
+        if (s + WPF < 8) X3_PIPE_V(3, 6, 12);
         else if (s < 7) X3_PIPE(6, 12);
         X3_SB();
-        if (s < 7) { b = bn; bn = bnn; a[0] = an[0]; a[1] = an[1]; }
+        if (s < 7) { a[0] = an[0]; a[1] = an[1]; }
       }
     }
 #pragma unroll
