@@ -366,12 +366,15 @@ __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetO
     __builtin_amdgcn_sched_barrier(0);  // one block's accumulators in VGPRs at a time
   }
   // lanes l and l ^ 32 hold the two halves of the same env's neurons; both lanes form the same sum
+  // (lower half + upper half: v_permlane32_swap of the partial with itself gives the lower half's
+  // value in every lane as the first result, the upper half's as the second -- a VALU swap, not an
+  // LDS permute)
 #pragma unroll
   for (int j = 0; j < NT; j++)
 #pragma unroll
     for (int q = 0; q < NOUT; q++) {
-      const float other = __shfl_xor(part[j][q], 32);
-      out[j][q] = ((h ? other : part[j][q]) + (h ? part[j][q] : other)) + L[o.w3 - 4 * h + NOUT * 128 + q];
+      const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(part[j][q]), __float_as_uint(part[j][q]), false, false);
+      out[j][q] = (__uint_as_float(p[0]) + __uint_as_float(p[1])) + L[o.w3 - 4 * h + NOUT * 128 + q];
     }
 }
 

@@ -49,7 +49,10 @@ __device__ __forceinline__ void fragments(const float ob[12], float (&xb)[NT][8]
   for (int k = 0; k < 8; k++) {
     const float lo = ob[k], hi = k < 4 ? ob[8 + k] : 0.f;  // this env's features k and 8 + k
     if constexpr (NT == 2) {  // lane l's env is tile (l >> 5)'s env l & 31
-      const float got = __shfl_xor(h ? lo : hi, 32);
+      // the other lane half's value (v_permlane32_swap: first result = lanes 0-31's, second = 32-63's)
+      const float x = h ? lo : hi;
+      const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+      const float got = __uint_as_float(h ? p[0] : p[1]);
       xb[0][k] = h ? got : lo;
       xb[NT - 1][k] = h ? hi : got;
     } else {  // both lane halves carry env l & 31
