@@ -110,6 +110,11 @@ __global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, c
 #define QD_X3_LOSS1 1
 #endif
 
+// L1: both tiles' MFMAs before either tile's ReLU / split / H1 image writes; 0 = tile by tile
+#ifndef QD_X3_L1BOTH
+#define QD_X3_L1BOTH 1
+#endif
+
 // how many k-steps ahead L2 / dh1 load their pre-split W2 pieces (global loads, L2-resident); round 5
 // A/B (profiles/r05/learner_wpf_ab.txt): 3 is 5 % slower (register pressure), 1 the same as 2
 #ifndef QD_X3_WPF
@@ -296,8 +301,35 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     LP(1);
 
     // ---- L1 (E form): h1^T block w of both tiles -> H1 pieces
+#if QD_X3_L1BOTH
+    // both tiles' operand reads and MFMAs first, then their ReLU / split / image writes (in program
+    // order per tile the compiler kept tile 1's reads behind tile 0's image stores)
+    f32x16 acc1[2];
+    {
+      X3 xb[2];
+#pragma unroll
+      for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int p = 0; p < 3; p++) xb[t].p[p] = rd16(XO, p * XIMG + (32 * t + l32) * XROW + 16 * h);
+      f32x16 sm[2];
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        acc1[0][r] = Lf[B_B1 / 4 + 32 * w + acc_row(r, h)];
+        sm[0][r] = 0.f;
+      }
+      acc1[1] = acc1[0];
+      sm[1] = sm[0];
+#pragma unroll
+      for (int t = 0; t < 2; t++) mma3s(w1x, xb[t], acc1[t], sm[t]);
+#pragma unroll
+      for (int t = 0; t < 2; t++) acc1[t] += sm[t];
+    }
+#endif
 #pragma unroll
     for (int t = 0; t < 2; t++) {
+#if QD_X3_L1BOTH
+      f32x16& acc = acc1[t];
+#else
       f32x16 acc;
 #pragma unroll
       for (int r = 0; r < 16; r++) acc[r] = Lf[B_B1 / 4 + 32 * w + acc_row(r, h)];
@@ -311,6 +343,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         mma3s(w1x, xb, acc, sm);
         acc += sm;
       }
+#endif
       if constexpr (DUMP) {
         LP_DUMP(if (valid[t])
           for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 0, 32 * w + acc_row(r, h), acc[r]));
