@@ -115,6 +115,11 @@ __global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, c
 #define QD_X3_L1BOTH 1
 #endif
 
+// relu'(h1)'s mask reads (H1 image) issued in dh1's last k-step; 0 = after dh1
+#ifndef QD_X3_MASKPF
+#define QD_X3_MASKPF 1
+#endif
+
 // how many k-steps ahead L2 / dh1 load their pre-split W2 pieces (global loads, L2-resident); round 5
 // A/B (profiles/r05/learner_wpf_ab.txt): 3 is 5 % slower (register pressure), 1 the same as 2
 #ifndef QD_X3_WPF
@@ -604,6 +609,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
     for (int r = 0; r < 16; r++) { dh1[0][r] = 0.f; dh1[1][r] = 0.f; }
     f32x16 dh1s[2] = {dh1[0], dh1[1]};
+#if QD_X3_MASKPF
+    s16x4 rmask[2][4];
+#endif
     {  // software pipeline as L2: A = DH2 row reads, B = pre-split W2 columns
       X3 a[2];
 #pragma unroll
@@ -620,6 +628,15 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
             for (int p = 0; p < 3; p++) an[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
         }
+#if QD_X3_MASKPF
+        if (s == 7) {  // relu'(h1)'s mask reads under the last k-step's MFMAs
+#pragma unroll
+          for (int t = 0; t < 2; t++)
+#pragma unroll
+            for (int gg = 0; gg < 4; gg++)
+              rmask[t][gg] = rdtr(L + B_H1P, soff(32 * t + 8 * gg + 4 * h + gq, 4 * w + tr_col) + tr_half);
+        }
+#endif
 #pragma unroll
         for (int t = 0; t < 2; t++) {
 #if defined(QD_X3_DH1ONE)
@@ -653,7 +670,11 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       // (h1 >= 0 after the ReLU: its top piece is > 0 exactly when h1 is a positive normal)
 #pragma unroll
       for (int gg = 0; gg < 4; gg++) {
+#if QD_X3_MASKPF
+        const s16x4 m = rmask[t][gg];
+#else
         const s16x4 m = rdtr(L + B_H1P, soff(32 * t + 8 * gg + 4 * h + gq, 4 * w + tr_col) + tr_half);
+#endif
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[4 * gg + q] = m[q] > 0 ? acc[4 * gg + q] : 0.f;
       }
