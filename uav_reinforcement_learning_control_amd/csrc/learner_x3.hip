@@ -120,6 +120,15 @@ __global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, c
 #define QD_X3_MASKPF 1
 #endif
 
+// dh1's first W2 pieces loaded in dW2's last k-step instead of after B4 (QD_X3_DH2OV only)
+#if !QD_X3_DH2OV
+#undef QD_X3_W1EARLY
+#define QD_X3_W1EARLY 0
+#endif
+#ifndef QD_X3_W1EARLY
+#define QD_X3_W1EARLY 0
+#endif
+
 // how many k-steps ahead L2 / dh1 load their pre-split W2 pieces (global loads, L2-resident); round 5
 // A/B (profiles/r05/learner_wpf_ab.txt): 3 is 5 % slower (register pressure), 1 the same as 2
 #ifndef QD_X3_WPF
@@ -558,6 +567,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     LP(9);
 #endif
 
+#if QD_X3_DH2OV
+    X3 wr1[WRING];  // dh1's W2 pieces (ring, WPF k-steps ahead)
+#endif
 #if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
     {  // 20 operand blocks (per k-step s: A, then B of jb = 0..3), each read one unit ahead
@@ -583,9 +595,19 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
           X3 an, bn;
           if (jb < 3) bn = trblk(B_H1P, s, 4 * (jb + 1) + tr_col);
           else if (s < 3) { an = trblk(B_DH2P, s + 1, 4 * w + tr_col); bn = trblk(B_H1P, s + 1, tr_col); }
+#if QD_X3_W1EARLY
+          if (s == 3 && jb == 0) {  // dh1's first W2 pieces, a k-step of dW2 ahead of B4
+#pragma unroll
+            for (int k = 0; k < WPF; k++) wr1[k] = WLOAD(1, k);
+          }
+#endif
           dW2[jb] = mma3(a, b, dW2[jb]);
 #if QD_X3_DH2OV
           if (s < 2 && (jb & 1) == 0) dh2_chunk(1, 2 * s + (jb >> 1));  // before (s = 1, jb = 3)'s k-step-2 reads
+#endif
+#if QD_X3_W1EARLY
+          if (s == 3 && jb == 0) X3_PIPE_V(3 * WPF, 6, 6);
+          else
 #endif
           if (jb < 3) X3_PIPE(6, 6);
           else if (s < 3) X3_PIPE(12, 6);
@@ -598,9 +620,10 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #endif
 #if QD_X3_DH2OV
     X3_BAR();  // B4: every wave's DH2 columns (dh1 reads whole rows)
-    X3 wr1[WRING];
+#if !QD_X3_W1EARLY
 #pragma unroll
     for (int k = 0; k < WPF; k++) wr1[k] = WLOAD(1, k);
+#endif
 #endif
     LP(10);
 #if !defined(QD_X3_NODH1)
