@@ -117,11 +117,11 @@ def _launch_floor_us(n_launch: int = 400) -> float:
 
 
 def _kernel_name(env) -> str:
-    """The step kernel form the handle actually launches (quad_kernel_form: lanes | 16 SPEC | 32 helper)."""
+    """The step kernel form the handle actually launches (quad_kernel_form: 16 SPEC | 32 helper waves |
+    128 256-env blocks | 256 nt | 512 k_step_hd)."""
     from uav_reinforcement_learning_control_amd import _native as N
     form = int(N.lib().quad_kernel_form(env._h))
-    lanes = form & 15
-    name = (f"k_step_g<{lanes}>" if lanes else ("k_step_h" if form & 32 else "k_step")) + "<HOVER,noCTBR>"
+    name = ("k_step_hd" if form & 512 else "k_step_h") + "<HOVER,noCTBR>"
     tags = (["SPEC constants"] if form & 16 else []) + (["helper waves draw the resets"] if form & 32 else []) + \
         (["nt state loads/stores"] if form & 256 else []) + (["7-wave DRAM form k_step_hd"] if form & 512 else [])
     return name + (f" ({', '.join(tags)})" if tags else "")
@@ -130,17 +130,14 @@ def _kernel_name(env) -> str:
 def _kernel_symbol(env) -> str:
     """The launched hover step kernel's template symbol as rocprofv3 names it (csrc/quadenv.hip
     quad_step_range: k_step_h<KIND, CTBR, SPEC, HB, NT> with HB from quad_kernel_form bit 7 (256-env
-    blocks for 32,769 .. 2,097,151 envs, else 64) and NT (the state's nt cache policy) from bit 8; k_step<KIND, CTBR, SPEC>; k_step_g<KIND, CTBR, G, SPEC>)."""
+    blocks for 32,769 .. 2,097,151 envs, else 64) and NT (the state's nt cache policy) from bit 8;
+    k_step_hd<KIND, CTBR, SPEC> when bit 9 is set)."""
     from uav_reinforcement_learning_control_amd import _native as N
     form = int(N.lib().quad_kernel_form(env._h))
-    lanes, spec = form & 15, "true" if form & 16 else "false"
-    if lanes:
-        return f"k_step_g<0, false, {lanes}, {spec}>"
+    spec = "true" if form & 16 else "false"
     if form & 512:
         return f"k_step_hd<0, false, {spec}>"
-    if form & 32:
-        return f"k_step_h<0, false, {spec}, {256 if form & 128 else 64}, {'true' if form & 256 else 'false'}>"
-    return f"k_step<0, false, {spec}>"
+    return f"k_step_h<0, false, {spec}, {256 if form & 128 else 64}, {'true' if form & 256 else 'false'}>"
 
 
 def _run_rank(args, rank, world, local_rank):
@@ -188,6 +185,7 @@ def _run_rank(args, rank, world, local_rank):
     if world > 1:
         dist.barrier()
     region_us = e0.elapsed_time(e1) * 1e3 / args.steps
+    own_elapsed = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -197,6 +195,9 @@ def _run_rank(args, rank, world, local_rank):
     res = dict(elapsed=elapsed, region_us=region_us,
                kernel_us=_gated_kernel_us(step, actions, args.kernel_launches),
                kernel=_kernel_name(env), symbol=_kernel_symbol(env), launch_floor_us=_launch_floor_us())
+    if world > 1:  # every rank's own figures: a slow GPU or link shows here, not only in the MAX
+        res["per_rank"] = _per_rank(dict(elapsed_s=own_elapsed, region_us=region_us, kernel_us=res["kernel_us"]),
+                                    ("elapsed_s", "region_us", "kernel_us"))
     if args.rollout_steps > 0:
         res["rollout"] = _rollout_phase(env, args)
     if args.e2e_iters > 0:
@@ -221,10 +222,46 @@ def _run_rank(args, rank, world, local_rank):
     return res
 
 
+def _mem_floor_fn(env):
+    """quad_mem_floor on the env's own tiles and output rows: the step's 278 B per env with no
+    compute, quad_step's cache policy for this size (the same-run memory floor of the step)."""
+    from uav_reinforcement_learning_control_amd import _native as N
+    L = N.lib()
+    out = N.QuadStepOut(obs=env.obs.data_ptr(), reward=env.reward.data_ptr(),
+                        terminated=env.terminated.data_ptr(), truncated=env.truncated.data_ptr())
+    h = env._h
+
+    def floor(actions_ptr: int):
+        s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        rc = L.quad_mem_floor(h, C.c_void_p(actions_ptr), C.byref(out), s)
+        if rc != 0:
+            N.check(rc, "quad_mem_floor")
+    return floor
+
+
+def _per_rank(mine: dict, keys) -> dict:
+    """Gather one dict of figures from every rank (all_gather_object, a collective: every rank calls
+    it); for each key in `keys` the per-rank list with min / max / argmax rank and max / min."""
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, dict(mine, rank=dist.get_rank()))
+    out = {"ranks": got}
+    for k in keys:
+        v = [g[k] for g in got]
+        if any(x is None for x in v):
+            continue
+        hi = max(range(len(v)), key=v.__getitem__)
+        out[k] = {"min": min(v), "max": v[hi], "argmax_rank": hi, "max_over_min": v[hi] / min(v) if min(v) > 0 else None}
+    return out
+
+
 def _large_point(n, dev, seed, launches) -> dict:
     """The same step at a large batch (the size's default kernel form) after 50 steps (the
     post-reset transient: ~11 % of envs reset per step from there on): gated per-launch time,
-    HBM roofline of the algorithmic bytes, and the committed PMC traffic of that kernel and size."""
+    HBM roofline of the algorithmic bytes, and the committed PMC traffic of that kernel and size.
+    Beside it, in the same process on the same buffers, the copy floor: quad_mem_floor's
+    per-launch time (the same loads and stores, no compute), timed the same way before and after
+    the step (their mean), so the step's distance from what this box's HBM delivers for its access
+    pattern is separated from the box-to-box spread of the absolute figure."""
     from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
     big = QuadVecEnv(n, env="hover", device=dev, seed=seed)
     big.reset()
@@ -232,15 +269,23 @@ def _large_point(n, dev, seed, launches) -> dict:
     st = _quad_step_fn(big)
     for k in range(50):
         st(acts[k % 8].data_ptr())
+    fl = _mem_floor_fn(big)
+    floor0 = _gated_kernel_us(fl, acts, launches)
     us = _gated_kernel_us(st, acts, launches)
+    floor1 = _gated_kernel_us(fl, acts, launches)
+    floor_us = 0.5 * (floor0 + floor1)
     sym = _kernel_symbol(big)
     big.close()
     del acts
     torch.cuda.empty_cache()
     gbs = BYTES_PER_ENV_STEP * n / (us * 1e-6) / 1e9
     return {"envs": n, "kernel_us": us, "env_steps_per_s_kernel": n / (us * 1e-6), "achieved_GBs": gbs,
-            "frac": gbs / HBM_PEAK_GBS, "kernel_symbol": sym, "traffic_pmc": _pmc_traffic(sym, n),
-            "issue": _pmc_issue(sym, n)}
+            "frac": gbs / HBM_PEAK_GBS, "copy_floor_us": floor_us, "copy_floor_us_before_after": [floor0, floor1],
+            "copy_floor_GBs": BYTES_PER_ENV_STEP * n / (floor_us * 1e-6) / 1e9,
+            "frac_of_copy_floor": floor_us / us,
+            "copy_floor_what": "quad_mem_floor: the step's 278 B/env of loads and stores on the same tiles "
+                               "and rows with quad_step's cache policy, no compute (same process, same buffers)",
+            "kernel_symbol": sym, "traffic_pmc": _pmc_traffic(sym, n), "issue": _pmc_issue(sym, n)}
 
 
 def _kernel_rate(n, kind, wrapper, dev, seed) -> dict:
@@ -278,8 +323,7 @@ def _kstep_rate(n, steps, dev, seed) -> dict:
     del r
     e.close()
     return {"envs": n, "steps_per_launch": steps,
-            "kernel": "k_step_random_h<HOVER,noCTBR> (helper waves draw actions and resets)"
-            if os.environ.get("QUADENV_HELPER", "1") != "0" else "k_step_random<HOVER,noCTBR>",
+            "kernel": "k_step_random_h<HOVER,noCTBR> (helper waves draw actions and resets)",
             "us_per_step": us, "env_steps_per_s": n / (us * 1e-6), "reset_fraction_per_step": resets,
             "bytes_per_env_step_out": 70, "note": "state read/written once per launch; actions drawn in-kernel"}
 
@@ -310,6 +354,13 @@ def _end_to_end(env, args, world: int = 1) -> dict:
     comm = m.comm_stats() if world > 1 else None
     steps = args.e2e_iters * rs.env_steps * world  # every rank's envs (config 4 at N = 8)
     wall = t_roll + t_train
+    per_rank = None
+    if world > 1:  # every rank's iteration and all-reduce figures (skew), then the slowest rank
+        per_rank = _per_rank(dict(wall_s=wall, rollout_s=t_roll / args.e2e_iters, train_s=t_train / args.e2e_iters,
+                                  allreduce_median_us=comm["median_us"] if comm else None,
+                                  allreduce_mean_us=comm["mean_us"] if comm else None,
+                                  allreduce_max_us=comm["max_us"] if comm else None),
+                             ("wall_s", "train_s", "allreduce_median_us", "allreduce_max_us"))
     if world > 1:  # the slowest rank sets the whole job's time
         t = torch.tensor([wall], dtype=torch.float64, device=env.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -329,6 +380,8 @@ def _end_to_end(env, args, world: int = 1) -> dict:
            "episodes_first_rollout": {"return_sum": first_stats[0], "length_sum": first_stats[1],
                                       "count": int(first_stats[2]), "local_count": first.extra["local_episodes"],
                                       "reduced_over_ranks": world > 1}}
+    if per_rank is not None:
+        out["per_rank"] = per_rank
     if world > 1:
         alone = _allreduce_alone(m)
         out["allreduce"] = dict(
@@ -851,6 +904,8 @@ def main():
                      "algorithmic_bytes_per_launch": BYTES_PER_ENV_STEP * args.envs,
                      "issue": _pmc_issue(res["symbol"], args.envs), **_launch_terms(res, args.envs)},
     }
+    if "per_rank" in res:
+        line["per_rank"] = res["per_rank"]
     if "rollout" in res:
         line["rollout_phase"] = res["rollout"]
     if "end_to_end" in res:

@@ -147,11 +147,10 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
                 int32_t n_envs, QuadHandle** out);
 void quad_destroy(QuadHandle* h);
 int32_t quad_num_envs(const QuadHandle* h);
-/* Diagnostics: the step-kernel form quad_create chose -- bits 0-3 lanes per env (0 = one thread
- * per env; 1/2/4 = k_step_g), bit 4 set when the handle's constant block is a reference default and
- * the kernels with compiled-in constants run (QUADENV_SPEC=0 turns that off), bit 5 set when the
- * one-thread form runs with helper waves drawing the resets (k_step_h; QUADENV_HELPER=0 turns it off),
- * bit 7 set when those helper blocks are 256 envs wide (full-batch steps of 32,769 .. 2,097,151 envs,
+/* Diagnostics: the step-kernel form quad_create chose -- bit 4 set when the handle's constant block
+ * is a reference default and the kernels with compiled-in constants run (QUADENV_SPEC=0 turns that
+ * off), bit 5 always set for the hover / trajectory kinds (one thread per env with helper waves
+ * drawing the resets, k_step_h; bits 0-3 were the lane-group forms removed in round 6), bit 7 set when those helper blocks are 256 envs wide (full-batch steps of 32,769 .. 2,097,151 envs,
  * or QUADENV_HBLOCK=256; 64-env blocks otherwise), bit 8 set when a full-batch step of those blocks
  * moves the env state with the nt cache policy (65,536-env-scale and >= 2M-env batches; QUADENV_NT
  * pins it), bit 9 set when those 64-env nt launches run as k_step_hd, the DRAM form with a
@@ -175,6 +174,15 @@ int quad_step(QuadHandle* h, const float* actions, const QuadStepOut* out, void*
  * overlap (one half's physics with the other half's memory traffic, or with a policy kernel). */
 int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* actions,
                     const QuadStepOut* out, void* stream);
+
+/* Measurement only (no reference counterpart; bench.py's live DRAM floor): the HBM traffic of one
+ * quad_step with no compute -- the same env tiles, actions and output rows, with quad_step's cache
+ * policy for this batch size: every env's 26 state words (qpos 11, qvel 10, voltage, target 3, step
+ * counter) read and written back unchanged, its action read, and obs [N,12], reward, terminated and
+ * truncated written (obs = the first 12 state words, reward = qpos[0], flags = 0). 278 bytes per env,
+ * quad_step's algorithmic bytes. The env state is left as it was; the output rows are overwritten.
+ * Hover / trajectory kinds without RELPOS. */
+int quad_mem_floor(QuadHandle* h, const float* actions, const QuadStepOut* out, void* stream);
 
 /* HoverEnv._get_obs for the current state (e.g. after quad_set_state). obs: device [N,12];
  * state12 (device [N,12] or NULL): the absolute QuadState vector (HoverEnv._state.vec()). */

@@ -151,17 +151,15 @@ def _pre12(st, i):
     return np.concatenate([st["qpos"][i][:3], np.zeros(3, np.float32), st["qvel"][i][:6]])
 
 
-@pytest.fixture(params=["1", "2", "4", "0", "0t", "0d", "0w", "0wt", "0n"])
+@pytest.fixture(params=["0", "0t", "0d", "0w", "0wt"])
 def kernel_variant(request, monkeypatch):
-    """Every step kernel form must be exact: k_step_g with 1, 2 or 4 lanes per env, and the
-    one-thread-per-env form (QUADENV_LANES=0) with helper waves drawing the resets (k_step_h, the
-    default at every size) -- in 64-env blocks ("0", the form up to 32,768 envs; "0t" with the nt
-    state cache policy, forced by QUADENV_NT: the form from 2M envs; "0d" the same as k_step_hd, the
-    7-waves-per-SIMD DRAM form of >= 4M-env batches, forced by QUADENV_HD) and in the 256-env blocks of
-    the batches between ("0w", forced by QUADENV_HBLOCK; "0wt" with the nt policy of the
-    65,536-env-scale batches) -- and without the helpers ("0n": k_step)."""
-    monkeypatch.setenv("QUADENV_LANES", request.param[0])
-    monkeypatch.setenv("QUADENV_HELPER", "0" if request.param.endswith("n") else "1")
+    """Every step kernel form must be exact: the one-thread-per-env step waves with helper waves
+    drawing the resets (k_step_h, the form at every size) -- in 64-env blocks ("0", the form up to
+    32,768 envs; "0t" with the nt state cache policy, forced by QUADENV_NT: the form from 2M envs; "0d"
+    the same as k_step_hd, the 7-waves-per-SIMD DRAM form of >= 4M-env batches, forced by QUADENV_HD)
+    and in the 256-env blocks of the batches between ("0w", forced by QUADENV_HBLOCK; "0wt" with the nt
+    policy of the 65,536-env-scale batches). (The one-wave k_step and the lane-group k_step_g forms
+    were A/B builds, removed from the library in round 6.)"""
     if "w" in request.param:
         monkeypatch.setenv("QUADENV_HBLOCK", "256")
     else:
@@ -189,7 +187,7 @@ def test_kernel_form_pins(monkeypatch):
     """QUADENV_HD / QUADENV_NT / QUADENV_HBLOCK pin the size policy (quad_create reads them); k_step_hd
     (bit 9) is only ever the 64-env nt launch: pinned on, it needs the nt policy and 64-env blocks."""
     from uav_reinforcement_learning_control_amd import _native as N
-    for v in ("QUADENV_HD", "QUADENV_NT", "QUADENV_HBLOCK", "QUADENV_LANES", "QUADENV_HELPER"):
+    for v in ("QUADENV_HD", "QUADENV_NT", "QUADENV_HBLOCK"):
         monkeypatch.delenv(v, raising=False)
     cases = ((1 << 22, dict(QUADENV_HD="0"), 32 | 256), (1 << 22, dict(QUADENV_NT="0"), 32),
              (1 << 22, dict(QUADENV_HBLOCK="256"), 32 | 128 | 256), (4096, dict(QUADENV_HD="1"), 32),
@@ -266,7 +264,7 @@ def test_step_matches_oracle_random_states(env_name, wrapper, kind, wrap, kernel
     nv, ov = operand_only(g["qvel"], np.stack([o["qvel"] for o in ref]), st["qvel"])
     ns, os_ = operand_only(g["state12"], np.stack([o["state12"] for o in ref]),
                            np.stack([_pre12(st, i) for i in range(n)]))
-    print(f"\noperand-relative-only components ({env_name}, {wrapper}, lanes {kernel_variant}, spec {spec_mode}): "
+    print(f"\noperand-relative-only components ({env_name}, {wrapper}, form {kernel_variant}, spec {spec_mode}): "
           f"qpos {nq}, qvel {nv}, state12 {ns} of {n} envs")
     assert len(oq) == len(ov) == len(os_) == 0, (oq[:5], ov[:5], os_[:5])
     assert nq + nv + ns <= 0.01 * n
@@ -296,7 +294,7 @@ def test_step_matches_reference_goldens(golden_dir, name, kind, wrap, ms, kernel
         assert parity_ok(g["qpos"][i], o["qpos"], st["qpos"][i]), i
     nq, oq = operand_only(g["qpos"], np.stack([o["qpos"] for o in ref]), st["qpos"])
     nv, ov = operand_only(g["qvel"], np.stack([o["qvel"] for o in ref]), st["qvel"])
-    print(f"\noperand-relative-only components ({name}, lanes {kernel_variant}): qpos {nq}, qvel {nv} of {n}")
+    print(f"\noperand-relative-only components ({name}, form {kernel_variant}): qpos {nq}, qvel {nv} of {n}")
     assert len(oq) == len(ov) == 0, (oq[:5], ov[:5])
     assert nq + nv <= max(1, 0.01 * n)
     env.close()
@@ -628,8 +626,8 @@ def test_ragged_sizes_match_oracle(n, kernel_variant):
 @pytest.mark.parametrize("n", [1000, 4096 + 37])
 def test_ragged_mass_auto_reset_draws(n, kernel_variant):
     """Every env truncates at once (max_episode_steps = 1) in a batch whose last wave is partly
-    empty: k_step computes the reset draws of a wave's resetting envs across ALL its lanes
-    (reset_words_wave), so lanes past N must take part. Each reset obs equals the oracle's draw."""
+    empty: k_step_h's helper waves draw every env's next-reset row, and the lanes past N shadow the
+    last env (in-range loads, no stores). Each reset obs equals the oracle's draw."""
     env = _env(n, seed=31, env_id_base=77, max_episode_steps=1)
     env.reset()
     cfg = O.default_cfg(O.ENV_HOVER, O.WRAP_NONE)
@@ -700,10 +698,9 @@ def test_invalid_arguments_fail_cleanly():
 
 
 @pytest.mark.parametrize("env_name,wrapper", [("hover", None), ("trajectory", "RateControlWrapper")])
-@pytest.mark.parametrize("helper", ["1", "1w", "0"])
+@pytest.mark.parametrize("helper", ["1", "1w"])
 def test_step_random_is_the_step_by_step_rollout(env_name, wrapper, spec_mode, helper, monkeypatch):
-    # k_step_random_h (default; "1w": its 256-env blocks of > 32,768-env batches) / k_step_random
-    monkeypatch.setenv("QUADENV_HELPER", helper[0])
+    # k_step_random_h ("1w": its 256-env blocks of > 32,768-env batches)
     if helper.endswith("w"):
         monkeypatch.setenv("QUADENV_HBLOCK", "256")
     else:

@@ -46,8 +46,6 @@ SEED, BASE = 0xC0FFEE, 1 << 20
 @pytest.fixture(params=["1", "0"])
 def spec_mode(request, monkeypatch):
     monkeypatch.setenv("QUADENV_SPEC", request.param)
-    monkeypatch.setenv("QUADENV_LANES", "0")
-    monkeypatch.setenv("QUADENV_HELPER", "1")
     monkeypatch.delenv("QUADENV_HBLOCK", raising=False)
     monkeypatch.delenv("QUADENV_NT", raising=False)
     return request.param

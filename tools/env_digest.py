@@ -20,12 +20,13 @@ def child(lib):
     import torch
     from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
     out = {}
-    forms = [("h64", dict(QUADENV_LANES="0", QUADENV_HELPER="1", QUADENV_HBLOCK="64")),
-             ("h256", dict(QUADENV_LANES="0", QUADENV_HELPER="1", QUADENV_HBLOCK="256")),
-             ("k", dict(QUADENV_LANES="0", QUADENV_HELPER="0", QUADENV_HBLOCK="64")),
-             ("g1", dict(QUADENV_LANES="1", QUADENV_HELPER="1", QUADENV_HBLOCK="64")),
-             ("g2", dict(QUADENV_LANES="2", QUADENV_HELPER="1", QUADENV_HBLOCK="64"))]
+    forms = [("h64", dict(QUADENV_HBLOCK="64", QUADENV_NT="0")),
+             ("h256", dict(QUADENV_HBLOCK="256", QUADENV_NT="0")),
+             ("h64nt", dict(QUADENV_HBLOCK="64", QUADENV_NT="1")),
+             ("hd", dict(QUADENV_HBLOCK="64", QUADENV_NT="1", QUADENV_HD="1"))]
     for fname, envs in forms:
+        for k in ("QUADENV_HBLOCK", "QUADENV_NT", "QUADENV_HD"):
+            os.environ.pop(k, None)
         os.environ.update(envs)
         for kind, wrapper in (("hover", None), ("hover", "RateControlWrapper"), ("trajectory", "RateControlWrapper")):
             h = hashlib.sha256()
@@ -40,8 +41,8 @@ def child(lib):
                 h.update(v.tobytes())
             e.close()
             out[f"step {fname} {kind} {wrapper}"] = h.hexdigest()[:16]
-    os.environ.update(QUADENV_LANES="0", QUADENV_HELPER="1")
-    os.environ.pop("QUADENV_HBLOCK", None)
+    for k in ("QUADENV_HBLOCK", "QUADENV_NT", "QUADENV_HD"):
+        os.environ.pop(k, None)
     from uav_reinforcement_learning_control_amd.ppo.fused import FusedPolicy
     from uav_reinforcement_learning_control_amd.ppo.policy import ActorCritic
     torch.manual_seed(0)

@@ -98,6 +98,7 @@ class QuadPolicyAct(C.Structure):
 # every symbol include/quadenv.h declares (checked by tests/test_abi.py)
 EXPORTS = ("quad_abi_version", "quad_last_error", "quad_default_cfg", "quad_create",
            "quad_destroy", "quad_num_envs", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe", "quad_terminated", "quad_step_random",
+           "quad_mem_floor",
            "quad_kernel_form", "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
            "quad_policy_packed_floats", "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
            "quad_waypoints_begin", "quad_waypoints_update", "quad_ppo_workspace_bytes", "quad_ppo_grad",
@@ -158,6 +159,7 @@ def _declare(L):
     L.quad_observe.argtypes = [vp, vp, vp, vp]
     L.quad_terminated.argtypes = [vp, vp, i32, vp, vp]
     L.quad_step_random.argtypes = [vp, u32, i32, C.POINTER(QuadStepOut), vp, vp]
+    L.quad_mem_floor.argtypes = [vp, vp, C.POINTER(QuadStepOut), vp]
     L.quad_kernel_form.argtypes = [vp]
     L.quad_kernel_form.restype = i32
     L.quad_random_actions.argtypes = [vp, u32, vp, vp]
@@ -188,6 +190,7 @@ def _declare(L):
     L.quad_adam_workspace_bytes.restype = C.c_int64
     L.quad_clip_adam.argtypes = [C.POINTER(QuadAdam), vp, C.c_int64, vp]
     for n in ("quad_clip_adam", "quad_ppo_grad", "quad_ppo_hidden", "quad_ppo_adv_stats", "quad_ppo_adv_stats_epoch", "quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe", "quad_terminated", "quad_step_random",
+           "quad_mem_floor",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
               "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
               "quad_waypoints_begin", "quad_waypoints_update"):

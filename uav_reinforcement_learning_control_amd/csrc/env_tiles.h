@@ -63,13 +63,6 @@ struct TilesA {
   }
   __device__ __forceinline__ float ld(int f, uint32_t vo) const { return __builtin_bit_cast(float, ldu(f, vo)); }
   __device__ __forceinline__ void st(int f, uint32_t vo, float x) const { stu(f, vo, __builtin_bit_cast(uint32_t, x)); }
-  // lane-varying field (k_step_g with G > 1): the whole offset in the VGPR
-  __device__ __forceinline__ float ldv(int f, uint32_t vo) const {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + uint32_t(f) * 256u, 0, AUX));
-  }
-  __device__ __forceinline__ void stv(int f, uint32_t vo, float x) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), r, vo + uint32_t(f) * 256u, 0, AUX);
-  }
 };
 using Tiles = TilesA<0>;
 template <typename T>
@@ -110,8 +103,8 @@ __device__ __forceinline__ void load_env(const KParams& p, int i, EnvRegs<float>
 }
 
 // the fields the physics and the observation need (not the voltage / CTBR integral: k_step_h's
-// helper waves own the control path; with STEP = false not the step counter either)
-template <int AUX = 0, bool STEP = true>
+// helper waves own the control path)
+template <int AUX = 0>
 __device__ __forceinline__ void load_env_motion(const KParams& p, int i, EnvRegs<float>& e) {
   const TilesA<AUX> S(p);
   const uint32_t o = env_off(uint32_t(i));
@@ -142,7 +135,7 @@ __device__ __forceinline__ uint32_t fresh_off(uint32_t o) {
   return o;
 }
 
-template <int AUX = 0, bool STEP = true>
+template <int AUX = 0>
 __device__ __forceinline__ void store_env(const KParams& p, int i, const EnvRegs<float>& e,
                                           bool ctbr) {
   const TilesA<AUX> S(p);
@@ -166,7 +159,7 @@ __device__ __forceinline__ void store_env(const KParams& p, int i, const EnvRegs
 #pragma unroll
     for (int j = 0; j < 3; j++) S.st(F_RINT + j, o, e.rint[j]);
   }
-  if (STEP) S.stu(F_STEP, o, uint32_t(e.step));
+  S.stu(F_STEP, o, uint32_t(e.step));
 }
 
 // Mark a loaded value as consumed here, before the step's first store. gfx9's vmcnt retires

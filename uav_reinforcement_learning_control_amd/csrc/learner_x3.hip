@@ -98,36 +98,11 @@ __global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, c
 
 
 
-// tile 1's dh2 in dW2's first k-steps (see the dh2 phase; round 5: 741-743 vs 755-759 us per
-// 524,288-row minibatch same-box, the same gradient bits; 0 = dh2 of both tiles, then B4, then dW2)
-#ifndef QD_X3_DH2OV
-#define QD_X3_DH2OV 1
-#endif
-
-// the loss terms one row per lane (each row once per wave instead of once per lane half), both
-// tiles' dL/d(head) by lane-half swaps; 0 = two rows per lane (every row on both halves)
-#ifndef QD_X3_LOSS1
-#define QD_X3_LOSS1 1
-#endif
-
-// L1: both tiles' MFMAs before either tile's ReLU / split / H1 image writes; 0 = tile by tile
-#ifndef QD_X3_L1BOTH
-#define QD_X3_L1BOTH 1
-#endif
-
-// relu'(h1)'s mask reads (H1 image) issued in dh1's last k-step; 0 = after dh1
-#ifndef QD_X3_MASKPF
-#define QD_X3_MASKPF 1
-#endif
-
-// dh1's first W2 pieces loaded in dW2's last k-step instead of after B4 (QD_X3_DH2OV only)
-#if !QD_X3_DH2OV
-#undef QD_X3_W1EARLY
-#define QD_X3_W1EARLY 0
-#endif
-#ifndef QD_X3_W1EARLY
-#define QD_X3_W1EARLY 0
-#endif
+// The schedule below is the one measured best (round 5, profiles/r05/learner_*_ab.txt; the not-kept
+// alternatives were A/B builds and are gone from the product source): L1 issues both tiles' MFMAs
+// before either tile's ReLU / split / image writes; the loss terms run one row per lane; tile 1's dh2
+// is computed in dW2's first k-steps (741-743 vs 755-759 us per 524,288-row minibatch same-box, the
+// same gradient bits); relu'(h1)'s mask reads are issued in dh1's last k-step.
 
 // how many k-steps ahead L2 / dh1 load their pre-split W2 pieces (global loads, L2-resident); round 5
 // A/B (profiles/r05/learner_wpf_ab.txt): 3 is 5 % slower (register pressure), 1 the same as 2
@@ -231,7 +206,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
   for (int k = 0; k < NOUT; k++) db3[k] = 0.f;
 #pragma unroll
   for (int k = 0; k < ACT; k++) dls[k] = 0.f;
-  [[maybe_unused]] const bool acc_lane = w == 0 && h == 0;  // QD_X3_LOSS1 0: one lane per row accumulates the per-row sums
 
   const int per_block = NOUT == ACT ? g.per_block : g.per_block_c;
   const int s0 = blk * per_block;
@@ -315,7 +289,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     LP(1);
 
     // ---- L1 (E form): h1^T block w of both tiles -> H1 pieces
-#if QD_X3_L1BOTH
     // both tiles' operand reads and MFMAs first, then their ReLU / split / image writes (in program
     // order per tile the compiler kept tile 1's reads behind tile 0's image stores)
     f32x16 acc1[2];
@@ -338,26 +311,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
       for (int t = 0; t < 2; t++) acc1[t] += sm[t];
     }
-#endif
 #pragma unroll
     for (int t = 0; t < 2; t++) {
-#if QD_X3_L1BOTH
       f32x16& acc = acc1[t];
-#else
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[r] = Lf[B_B1 / 4 + 32 * w + acc_row(r, h)];
-      X3 xb;
-#pragma unroll
-      for (int p = 0; p < 3; p++) xb.p[p] = rd16(XO, p * XIMG + (32 * t + l32) * XROW + 16 * h);
-      {
-        f32x16 sm;
-#pragma unroll
-        for (int r = 0; r < 16; r++) sm[r] = 0.f;
-        mma3s(w1x, xb, acc, sm);
-        acc += sm;
-      }
-#endif
       if constexpr (DUMP) {
         LP_DUMP(if (valid[t])
           for (int r = 0; r < 16; r++) dump_pre(g.dump, NOUT == ACT ? 0 : 1, g.batch, base + 32 * t + l32, 0, 32 * w + acc_row(r, h), acc[r]));
@@ -457,7 +413,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 
     // ---- per-row loss terms and dL/d(head output) (every wave, identical arithmetic)
     float d[2][NOUT];
-#if QD_X3_LOSS1
     // one row per lane (row = lane: tile h, row l32), then both tiles' d on every lane by one
     // v_permlane32_swap per output; the per-row sums accumulate on every lane of wave 0
     {
@@ -465,14 +420,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       const bool vrow = h ? valid[1] : valid[0];
       const bool acc = w == 0 && vrow;
       float dd[NOUT];
-#else
-#pragma unroll
-    for (int t = 0; t < 2; t++) {
-      const int e = 32 * t + l32;
-      const bool vrow = valid[t];
-      const bool acc = acc_lane && vrow;
-      float (&dd)[NOUT] = d[t];
-#endif
       const float* PT = Lf + B_PART / 4;
       float out[NOUT];
 #pragma unroll
@@ -508,7 +455,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         dd[0] = vrow ? 2.f * g.vf_coef * g.inv_batch * diff : 0.f;
         st[1] = acc ? st[1] + diff * diff : st[1];
       }
-#if QD_X3_LOSS1
 #pragma unroll
       for (int k = 0; k < NOUT; k++) {
         db3[k] = w == 0 ? db3[k] + dd[k] : db3[k];
@@ -516,10 +462,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         d[0][k] = __uint_as_float(p[0]);  // lanes 0-31's value (tile 0's row) in every lane
         d[1][k] = __uint_as_float(p[1]);  // lanes 32-63's (tile 1's)
       }
-#else
-#pragma unroll
-      for (int k = 0; k < NOUT; k++) db3[k] = acc_lane ? db3[k] + dd[k] : db3[k];
-#endif
     }
     LP(7);
     // ---- dh2 (E form) -> DH2 pieces; dW3 per lane
@@ -544,7 +486,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
       for (int p = 0; p < 3; p++) *reinterpret_cast<bf16x4*>(L + B_DH2P + p * IMG + off) = x.p[p];
     };
-#if QD_X3_DH2OV
     // dW2 reads only this wave's own DH2 columns (its neurons) and the H1 image (complete since
     // B2), so it needs no barrier: tile 0's dh2 first, then dW2's first two k-steps (rows 0..31 =
     // tile 0) with tile 1's dh2 chunks in their issue gaps, written before the k-step-2 reads of
@@ -554,23 +495,13 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     for (int gg = 0; gg < 4; gg++) dh2_chunk(0, gg);
     LP(8);
     LP(9);
-#else
-#pragma unroll
-    for (int t = 0; t < 2; t++)
-#pragma unroll
-      for (int gg = 0; gg < 4; gg++) dh2_chunk(t, gg);
-    LP(8);
-    X3_BAR();  // B4: DH2 image complete
-    X3 wr1[WRING];  // dh1's first WPF k-steps: in flight through dW2
-#pragma unroll
-    for (int k = 0; k < WPF; k++) wr1[k] = WLOAD(1, k);
-    LP(9);
-#endif
 
-#if QD_X3_DH2OV
     X3 wr1[WRING];  // dh1's W2 pieces (ring, WPF k-steps ahead)
-#endif
-#if !defined(QD_X3_NODW2)  // QD_X3_*: cost-ablation builds only
+#if defined(QD_X3_NODW2)  // QD_X3_NO*: cost-ablation builds only (tools/x3_build.sh)
+    // without dW2 tile 1's dh2 still has to be written before B4 (dh1 reads its rows)
+#pragma unroll
+    for (int gg = 0; gg < 4; gg++) dh2_chunk(1, gg);
+#else
     // ---- dW2 slab (rows 32w..): K = the round's 64 rows, both operands by transposed reads
     {  // 20 operand blocks (per k-step s: A, then B of jb = 0..3), each read one unit ahead
       // The K order over the rows is free (both operands use it): the 4-row blocks of the transposed
@@ -595,20 +526,8 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
           X3 an, bn;
           if (jb < 3) bn = trblk(B_H1P, s, 4 * (jb + 1) + tr_col);
           else if (s < 3) { an = trblk(B_DH2P, s + 1, 4 * w + tr_col); bn = trblk(B_H1P, s + 1, tr_col); }
-#if QD_X3_W1EARLY
-          if (s == 3 && jb == 0) {  // dh1's first W2 pieces, a k-step of dW2 ahead of B4
-#pragma unroll
-            for (int k = 0; k < WPF; k++) wr1[k] = WLOAD(1, k);
-          }
-#endif
           dW2[jb] = mma3(a, b, dW2[jb]);
-#if QD_X3_DH2OV
           if (s < 2 && (jb & 1) == 0) dh2_chunk(1, 2 * s + (jb >> 1));  // before (s = 1, jb = 3)'s k-step-2 reads
-#endif
-#if QD_X3_W1EARLY
-          if (s == 3 && jb == 0) X3_PIPE_V(3 * WPF, 6, 6);
-          else
-#endif
           if (jb < 3) X3_PIPE(6, 6);
           else if (s < 3) X3_PIPE(12, 6);
           X3_SB();
@@ -618,13 +537,9 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       }
     }
 #endif
-#if QD_X3_DH2OV
     X3_BAR();  // B4: every wave's DH2 columns (dh1 reads whole rows)
-#if !QD_X3_W1EARLY
 #pragma unroll
     for (int k = 0; k < WPF; k++) wr1[k] = WLOAD(1, k);
-#endif
-#endif
     LP(10);
 #if !defined(QD_X3_NODH1)
     // ---- dh1 (R form) = relu'(h1) . (dh2 W2[:, block w]); then the dW1 slab (+ db1 in column 12)
@@ -632,9 +547,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
     for (int r = 0; r < 16; r++) { dh1[0][r] = 0.f; dh1[1][r] = 0.f; }
     f32x16 dh1s[2] = {dh1[0], dh1[1]};
-#if QD_X3_MASKPF
     s16x4 rmask[2][4];
-#endif
     {  // software pipeline as L2: A = DH2 row reads, B = pre-split W2 columns
       X3 a[2];
 #pragma unroll
@@ -651,7 +564,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
 #pragma unroll
             for (int p = 0; p < 3; p++) an[t].p[p] = rd16(L, B_DH2P + p * IMG + soff(32 * t + l32, s + 1 + 8 * h));
         }
-#if QD_X3_MASKPF
         if (s == 7) {  // relu'(h1)'s mask reads under the last k-step's MFMAs
 #pragma unroll
           for (int t = 0; t < 2; t++)
@@ -659,7 +571,6 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
             for (int gg = 0; gg < 4; gg++)
               rmask[t][gg] = rdtr(L + B_H1P, soff(32 * t + 8 * gg + 4 * h + gq, 4 * w + tr_col) + tr_half);
         }
-#endif
 #pragma unroll
         for (int t = 0; t < 2; t++) {
 #if defined(QD_X3_DH1ONE)
@@ -693,11 +604,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
       // (h1 >= 0 after the ReLU: its top piece is > 0 exactly when h1 is a positive normal)
 #pragma unroll
       for (int gg = 0; gg < 4; gg++) {
-#if QD_X3_MASKPF
         const s16x4 m = rmask[t][gg];
-#else
-        const s16x4 m = rdtr(L + B_H1P, soff(32 * t + 8 * gg + 4 * h + gq, 4 * w + tr_col) + tr_half);
-#endif
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[4 * gg + q] = m[q] > 0 ? acc[4 * gg + q] : 0.f;
       }
@@ -761,7 +668,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
     for (int o = 16; o > 0; o >>= 1) x += __shfl_xor(x, o);
     if (l32 == 0) P[P_B2 + 32 * w + acc_row(r, h)] = x;
   }
-  if (w == 0) {  // the per-row sums (QD_X3_LOSS1: on every lane; else lanes 0..31, zeros above)
+  if (w == 0) {  // the per-row sums (one row per lane: every lane of wave 0 holds some)
     float v[NOUT + ACT + 3];
     int nv = 0;
 #pragma unroll

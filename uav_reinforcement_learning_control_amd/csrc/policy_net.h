@@ -81,12 +81,9 @@ __device__ __forceinline__ void bias_init(f32x16& acc, const float* L, int off) 
 // 1/16 of one 32-neuron block's head: ReLU of accumulator register(s) `i` (actor: register i; critic:
 // registers 4(i/4).. handled at i % 4 == 0) times the packed head weights, into part[][].
 // (o3 = NET_W3 + 4h: the lane's part of the head-weight region)
-// QD_HEAD_PK: the actor head's four FMAs per hidden value as two v_pk_fma_f32 (each lane of a
-// packed FMA is the same fused multiply-add, so the same bits, tools/env_digest.py); 0 = four
-// v_fma_f32. Round 4 A/B (k_rollout, 65,536 envs): 27.63 / 27.74 vs 27.73 / 27.93 us per step
-#ifndef QD_HEAD_PK
-#define QD_HEAD_PK 1
-#endif
+// The actor head's four FMAs per hidden value as two v_pk_fma_f32 (each lane of a packed FMA is the
+// same fused multiply-add, so the same bits as four v_fma_f32, tools/env_digest.py). Round 4 A/B
+// (k_rollout, 65,536 envs): 27.63 / 27.74 vs 27.73 / 27.93 us per step for the four plain FMAs
 template <int NOUT, int NT>
 __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32x16 (&x)[NT], int m, int i,
                                           int o3, float (&part)[NT][NOUT]) {
@@ -95,18 +92,11 @@ __device__ __forceinline__ void head_part(const float* __restrict__ L, const f32
 #pragma unroll
     for (int j = 0; j < NT; j++) {
       const float v = relu(x[j][i]);
-#if QD_HEAD_PK
       const f32x2 vv = {v, v}, w01 = {w.x, w.y}, w23 = {w.z, w.w};
       f32x2 p01 = {part[j][0], part[j][1]}, p23 = {part[j][2], part[j][3]};
       p01 = __builtin_elementwise_fma(w01, vv, p01);
       p23 = __builtin_elementwise_fma(w23, vv, p23);
       part[j][0] = p01[0]; part[j][1] = p01[1]; part[j][2] = p23[0]; part[j][3] = p23[1];
-#else
-      part[j][0] = fmaf(w.x, v, part[j][0]);
-      part[j][1] = fmaf(w.y, v, part[j][1]);
-      part[j][2] = fmaf(w.z, v, part[j][2]);
-      part[j][3] = fmaf(w.w, v, part[j][3]);
-#endif
     }
   } else {
     if (i % 4 != 0) return;
@@ -178,10 +168,9 @@ __device__ __forceinline__ P3 ld_split8(const float* L, int off) {
 // per-net LDS offsets of this lane (floats), opaque to the compiler: every read is one of these
 // plus an immediate (< 64 KB). Left to itself it hoists one address register per distinct offset out
 // of the callers' step loops (the critic's image starts 76 KB into the LDS) -- ~100 of them, spilled.
-// VALU per MFMA in each step's interleave (A/B builds of tools/diag/net_bench.hip; 0: the scheduler's own order)
-#ifndef QD_NF_VPG
-#define QD_NF_VPG 5
-#endif
+// VALU per MFMA in each step's interleave (measured on tools/diag/net_bench.hip builds; the
+// scheduler's own order without the group barriers was slower)
+constexpr int NF_VPG = 5;
 typedef __attribute__((address_space(1))) const bf16x8 gbf16x8;  // global loads, not flat
 struct NetOff {
   int w1, w2, b, w3;
@@ -344,13 +333,11 @@ __device__ __forceinline__ void net_core(const float* __restrict__ L, const NetO
         }
       }
       hook(g);
-#if QD_NF_VPG > 0
 #pragma unroll
       for (int q = 0; q < 6 * NT; q++) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, QD_NF_VPG, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, NF_VPG, 0);
       }
-#endif
       __builtin_amdgcn_sched_barrier(0);
     }
   }

@@ -8,8 +8,10 @@
 // are transposed through LDS so that each wave-store instruction writes 1 KiB contiguously.
 //
 // Kernels
-//   k_step<KIND, CTBR>   fused: (CTBR) -> mixer -> voltage -> mj_step -> obs -> reward ->
-//                        termination/truncation -> SB3 auto-reset -> obs (LDS transpose)
+//   k_step_h<KIND, CTBR> fused: (CTBR) -> mixer -> voltage -> mj_step -> obs -> reward ->
+//   (k_step_hd)          termination/truncation -> SB3 auto-reset -> obs, with helper waves
+//                        (control path, next-reset rows); k_step_hd: its >= 4M-env DRAM form
+//   k_step_random_h      config 2: K random-action steps per launch
 //   k_reset<KIND>        HoverEnv.reset for all / masked envs
 //   k_observe            HoverEnv._get_obs of the current state
 //   k_random_actions     action_space.sample() stand-in (Philox), config 2
@@ -23,7 +25,6 @@
 #include <string>
 
 #include "../../include/quadenv.h"
-#include "quad_lanes.h"
 #include "quad_model.h"
 #include "quad_physics.h"
 #include "env_tiles.h"
@@ -78,46 +79,6 @@ __device__ __forceinline__ void reset_env(const KParams& p, int i, EnvRegs<float
   env_reset_from<float, KIND>(*p.kc, e, init12, tgt, obs, s12);
 }
 
-// The reset draws of a wave's resetting envs, compacted: each resetting lane publishes (env,
-// episode) under its rank among them, every lane of the wave then computes one (env, block) Philox
-// item, and the resetting lanes read back their 16 words. With <= 16 resets per wave (the common
-// case) that is one Philox pass for the wave instead of four serial ones per resetting lane: a
-// Philox block is 20 quarter-rate v_mad_u64_u32, and the draw was half the reset branch.
-// Identical words to reset_draw (same counters), handed back as the uniforms u01(word): converted
-// by the lane that made the block, 4 per lane instead of 16 in each resetting lane's stream.
-// Called by every active lane of the wave.
-struct ResetLds {
-  uint32_t env[4][64], ep[4][64];
-  float4 words[4][256];  // [wave][rank * 4 + block]
-};
-__device__ __forceinline__ void reset_words_wave(const KParams& p, ResetLds& L, uint32_t i, uint32_t ep,
-                                                 bool rs, float u16[16]) {
-  const uint64_t m = __ballot(rs);
-  if (m == 0) return;
-  const int w = threadIdx.x >> 6, lane = __lane_id();
-  const int nres = __popcll(m);
-  const int rank = __popcll(m & __lanemask_lt());
-  if (rs) { L.env[w][rank] = i; L.ep[w][rank] = ep; }
-  __builtin_amdgcn_wave_barrier();
-  const int passes = (nres * 4 + 63) >> 6;
-  for (int t = 0; t < passes; t++) {
-    const int item = t * 64 + lane, rr = item >> 2;
-    if (rr < nres) {
-      uint32_t c[4];
-      reset_block(p.seed, p.gid_base + uint64_t(L.env[w][rr]), L.ep[w][rr], uint32_t(item & 3), c);
-      L.words[w][item] = make_float4(u01(c[0]), u01(c[1]), u01(c[2]), u01(c[3]));
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (rs) {
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const float4 v = L.words[w][rank * 4 + b];
-      u16[4 * b] = v.x; u16[4 * b + 1] = v.y; u16[4 * b + 2] = v.z; u16[4 * b + 3] = v.w;
-    }
-  }
-}
-
 // One 12-float row per lane: three 16-byte stores when the row base is 16-byte aligned (a uniform
 // test), else twelve dword stores. Row-per-lane stores are issue-bound: 12 scattered dword
 // stores per lane cost the wave far more issue time than 3 dwordx4.
@@ -130,24 +91,6 @@ __device__ __forceinline__ void store_row12(float* __restrict__ base, uint32_t i
   } else {
 #pragma unroll
     for (int j = 0; j < 12; j++) sto(base, 48u * i + 4u * j, v[j]);
-  }
-}
-
-// Stage the block's [256,12] obs rows through LDS; write them as contiguous float4.
-__device__ __forceinline__ void store_obs_rows(float4* lds, const float obs[12], float* out,
-                                               int block_first, int n) {
-  const int t = threadIdx.x;
-  lds[3 * t + 0] = make_float4(obs[0], obs[1], obs[2], obs[3]);
-  lds[3 * t + 1] = make_float4(obs[4], obs[5], obs[6], obs[7]);
-  lds[3 * t + 2] = make_float4(obs[8], obs[9], obs[10], obs[11]);
-  __syncthreads();
-  const int rows = min(BLOCK, n - block_first);
-  const int nf4 = rows * 3;
-  float4* dst = reinterpret_cast<float4*>(out + size_t(block_first) * 12);
-#pragma unroll
-  for (int j = 0; j < 3; j++) {
-    const int idx = j * BLOCK + t;
-    if (idx < nf4) dst[idx] = lds[idx];
   }
 }
 
@@ -166,114 +109,6 @@ __device__ __forceinline__ void target_info_of(const KConsts<float>& K, const KP
 __device__ __forceinline__ void store_target_info(float* __restrict__ out, int i, const float o[9]) {
 #pragma unroll
   for (int j = 0; j < 9; j++) sto(out, uint32_t(i) * 36u + 4u * j, o[j]);
-}
-
-// The step of one env per thread; K is the handle's constant block (k_step's SPEC form passes a
-// compile-time copy of the default block, so every constant is an immediate).
-template <int KIND, bool CTBR>
-__device__ __forceinline__ void step_body(const KConsts<float>& K, KParams p, const float4* __restrict__ act,
-                                          QuadStepOut out, float4* lds, ResetLds& rl) {
-  const int block_first = p.first + blockIdx.x * BLOCK;
-  const int end = p.first + p.count;
-  // Every thread runs the step: the reset draws are computed by the whole wave (reset_words_wave),
-  // so lanes past the last env shadow it (in-range loads) and store nothing.
-  const bool live = block_first + int(threadIdx.x) < end;
-  const int i = live ? block_first + int(threadIdx.x) : end - 1;
-  float obs[12];
-#if defined(QD_PROBE)
-  uint64_t stamp_buf[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t* stamps = out.target_info ? stamp_buf : nullptr;  // probe builds: target_info = stamp buffer
-  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-  bool rs_probe = false;
-#else
-  uint64_t* stamps = nullptr;
-#endif
-  QD_STAMP(stamps, 0);
-  {
-    EnvRegs<float> e;
-    load_env(p, i, e, CTBR);
-    const Tiles S(p);
-    const uint32_t vo = env_off(uint32_t(i));
-    const uint32_t ep = S.ldu(F_EP, vo);
-    const float4 a4 = act[i];
-    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
-#if defined(QD_PROBE)
-    if (stamps) {  // stamp 1: every load of the step has landed
-      settle(ep); settle(__builtin_bit_cast(uint32_t, a4.x)); settle(__builtin_bit_cast(uint32_t, e.volt));
-      settle(__builtin_bit_cast(uint32_t, e.s[3])); settle(uint32_t(e.step)); settle(__builtin_bit_cast(uint32_t, e.target[2]));
-    }
-#endif
-    QD_STAMP(stamps, 1);
-    StepRes r;
-    env_step<float, CTBR>(K, e, a, r, stamps);
-    QD_STAMP(stamps, 5);
-    settle(ep);
-    const uint32_t o = uint32_t(i) * 4u;
-#if defined(QD_PROBE)
-    if (live && !stamps) {
-#else
-    if (live) {
-#endif
-      sto(out.reward, o, r.reward);
-      sto(out.terminated, uint32_t(i), uint8_t(r.term));
-      sto(out.truncated, uint32_t(i), uint8_t(r.trunc));
-      if (out.motor_commands)
-        sto(reinterpret_cast<float4*>(out.motor_commands), 4u * o,
-            make_float4(r.motor[0], r.motor[1], r.motor[2], r.motor[3]));
-      if (out.voltage_scale) sto(out.voltage_scale, o, r.vscale);
-      if (out.state12) store_row12(out.state12, uint32_t(i), r.state12);
-      if (out.target_info) {
-        float info[9];
-        target_info_of<KIND>(K, p, i, e, ep, info);
-        store_target_info(out.target_info, i, info);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
-#if defined(QD_ABL_NORESET)
-    const bool rs = false;
-#else
-    const bool rs = live && (r.term || r.trunc) && p.auto_reset;
-#endif
-#if defined(QD_PROBE)
-    rs_probe = rs;
-#endif
-    float u16[16];
-#if defined(QD_ABL_NODRAW)  // cost ablation (tools only): the reset without its Philox draw / LDS hand-off
-#pragma unroll
-    for (int j = 0; j < 16; j++) u16[j] = 0.5f;
-#else
-    reset_words_wave(p, rl, uint32_t(i), ep, rs, u16);
-#endif
-    if (stamps && rs) QD_PIN_N(u16, 16);
-    QD_STAMP(stamps, 8);
-    if (rs) {
-      if (out.terminal_obs) store_row12(out.terminal_obs, uint32_t(i), r.obs);
-      QD_STAMP(stamps, 9);
-      float init12[12], tgt[3], s12[12];
-      reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
-      env_reset_from<float, KIND>(K, e, init12, tgt, obs, s12);
-      if (stamps) { QD_PIN_N(obs, 12); QD_PIN_N(e.q, 4); }
-      QD_STAMP(stamps, 10);
-      S.stu(F_EP, vo, ep + 1u);
-    }
-    if (stamps) { QD_PIN_N(obs, 12); QD_PIN_N(e.q, 4); QD_PIN_N(e.pos, 3); }
-    QD_STAMP(stamps, 6);
-    if (live) store_env(p, i, e, CTBR);
-  }
-  store_obs_rows(lds, obs, out.obs, block_first, p.first + p.count);
-#if defined(QD_PROBE)
-  QD_STAMP(stamps, 7);
-  if (stamps && (threadIdx.x & 63) == 0) {
-    const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
-    uint64_t* dst = reinterpret_cast<uint64_t*>(out.target_info) + size_t(block_first + int(threadIdx.x)) / 64 * 16;
-#pragma unroll
-    for (int k = 0; k < 12; k++) dst[k] = stamp_buf[k];
-    dst[12] = rt0; dst[13] = rt1;
-    dst[14] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID (id 20)
-    dst[15] = __popcll(__ballot(rs_probe));
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -570,12 +405,18 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #endif
 }
 
+// SPEC: the handle's constant block equals the reference default (quad_create checks the bytes), so
+// the constants are compiled in -- no scalar loads of the block and no waits on them inside the step.
+// Kernel-argument preload (csrc/Makefile: -amdgpu-kernarg-preload-count=16): the leading scalar
+// arguments -- what the state loads need: tiles, their size, the env range, the actions -- arrive
+// in SGPRs at wave launch, so the loads are issued without first waiting on a scalar load of the
+// kernarg segment (the KParams / QuadStepOut aggregates behind them are not preloaded).
 template <int KIND, bool CTBR, bool SPEC, int HB, bool NT>
 __global__ __launch_bounds__(2 * HB) void k_step_h(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
                                                       int32_t first, int32_t count,
                                                       const KConsts<float>* __restrict__ kc, KParams p, QuadStepOut out) {
-  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
-  p.kc = kc;
+  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (above)
+  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
   __shared__ float4 lds[HB * 3];
   __shared__ __attribute__((aligned(16))) float H[HROW * HB];
   __shared__ __attribute__((aligned(16))) float CT[(ct_rows<CTBR>() ? CT_STRIDE : (CTBR ? HCTL : HCTL - 3)) * HB];
@@ -599,7 +440,7 @@ template <int KIND, bool CTBR, bool SPEC>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(7, 8)))
 void k_step_hd(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes, int32_t first, int32_t count,
                const KConsts<float>* __restrict__ kc, KParams p, QuadStepOut out) {
-  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
+  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step_h)
   p.kc = kc;
   __shared__ float4 lds[64 * 3];
   __shared__ __attribute__((aligned(16))) float H[HROW * 64];
@@ -612,94 +453,50 @@ void k_step_hd(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes
   }
 }
 
-// k_step: one env per thread. SPEC: the handle's constant block equals the reference default
-// (quad_create checks the bytes), so the constants are compiled in -- no scalar loads of the block
-// and no waits on them inside the step.
-// Kernel-argument preload (csrc/Makefile: -amdgpu-kernarg-preload-count=16): the leading scalar
-// arguments -- what the state loads need: tiles, their size, the env range, the actions -- arrive
-// in SGPRs at wave launch, so the loads are issued without first waiting on a scalar load of the
-// kernarg segment (the KParams / QuadStepOut aggregates behind them are not preloaded).
-template <int KIND, bool CTBR, bool SPEC>
-__global__ __launch_bounds__(BLOCK) void k_step(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
-                                                int32_t first, int32_t count, const KConsts<float>* __restrict__ kc,
-                                                KParams p, QuadStepOut out) {
-  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;
-  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores below (see KParams)
-  __shared__ float4 lds[BLOCK * 3];
-  __shared__ ResetLds rl;
-  if constexpr (SPEC) {
-    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
-    step_body<KIND, CTBR>(K, p, act, out, lds, rl);
-  } else {
-    step_body<KIND, CTBR>(*kc, p, act, out, lds, rl);
-  }
+// quad_mem_floor: the step's loads and stores with no compute (bench.py's live DRAM floor). One env
+// per lane, 256-env blocks, the state through the same buffer resource and cache policy (AUX) as
+// k_step_h's tiles; obs rows as three dwordx4 per lane (a wave's rows are contiguous).
+template <int AUX>
+__global__ __launch_bounds__(256) void k_mem_floor(KParams p, const float4* __restrict__ act, QuadStepOut out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.n) return;
+  const TilesA<AUX> S(p);
+  const uint32_t o = env_off(uint32_t(i));
+  uint32_t x[26];
+#pragma unroll
+  for (int f = 0; f < 25; f++) x[f] = S.ldu(f, o);
+  x[25] = S.ldu(F_STEP, o);
+  const float4 a = act[i];
+  // the action feeds the flags (false for any finite action), so its load is not dead
+  const bool big = !(fabsf(a.x + a.y + a.z + a.w) < 1e30f);
+  const uint32_t q = fresh_off(o);
+#pragma unroll
+  for (int f = 0; f < 25; f++) S.stu(f, q, x[f]);
+  S.stu(F_STEP, q, x[25]);
+  float4* ob = reinterpret_cast<float4*>(out.obs) + size_t(i) * 3;
+#pragma unroll
+  for (int j = 0; j < 3; j++)
+    ob[j] = make_float4(__uint_as_float(x[4 * j]), __uint_as_float(x[4 * j + 1]), __uint_as_float(x[4 * j + 2]),
+                        __uint_as_float(x[4 * j + 3]));
+  out.reward[i] = __uint_as_float(x[0]);
+  out.terminated[i] = big;
+  out.truncated[i] = big;
 }
-
 
 // Config 2 of the scope table -- debug_training.py:111's loop env.step(env.action_space.sample())
-// -- as ONE launch: `steps` whole k_step steps per thread with the action of step s drawn in-kernel
-// from quad_random_actions' map, Philox(seed; gid, step0 + s, 0x100), and the env state kept in
-// registers between steps (read once, written once). Per step every output row goes to HBM as in
-// k_step: obs [N,12] through the block's LDS transpose, reward, flags, terminal obs of finishing
-// envs, all time-major [steps][N, ...]. Same env_step code as k_step, so the same bits.
-template <int KIND, bool CTBR>
-__device__ __forceinline__ void step_random_body(const KConsts<float>& K, KParams p, QuadStepOut out,
-                                                 float4* __restrict__ act_out, uint32_t step0, int32_t steps,
-                                                 float4* lds, ResetLds& rl) {
-  const int block_first = blockIdx.x * BLOCK;
-  const int n = p.n;
-  const bool live = block_first + int(threadIdx.x) < n;
-  const int i = live ? block_first + int(threadIdx.x) : n - 1;  // shadow lanes: in-range, store nothing
-  EnvRegs<float> e;
-  load_env(p, i, e, CTBR);
-  const Tiles S(p);
-  const uint32_t vo = env_off(uint32_t(i));
-  uint32_t ep = S.ldu(F_EP, vo);
-  const uint64_t gid = p.gid_base + uint64_t(i);
-  for (int t = 0; t < steps; t++) {
-    uint32_t c[4] = {uint32_t(gid), uint32_t(gid >> 32), step0 + uint32_t(t), 0x100u};
-    philox4x32_10(c, uint32_t(p.seed), uint32_t(p.seed >> 32));
-    const float a[4] = {float(c[0] >> 8) * 0x1p-23f - 1.0f, float(c[1] >> 8) * 0x1p-23f - 1.0f,
-                        float(c[2] >> 8) * 0x1p-23f - 1.0f, float(c[3] >> 8) * 0x1p-23f - 1.0f};
-    StepRes r;
-    env_step<float, CTBR>(K, e, a, r);
-    const uint32_t row = uint32_t(t) * uint32_t(n) + uint32_t(i);  // time-major row (< 2^32: checked)
-    if (live) {
-      sto(out.reward, 4u * row, r.reward);
-      sto(out.terminated, row, uint8_t(r.term));
-      sto(out.truncated, row, uint8_t(r.trunc));
-      if (act_out) sto(act_out, 16u * row, make_float4(a[0], a[1], a[2], a[3]));
-    }
-    float obs[12];
-#pragma unroll
-    for (int j = 0; j < 12; j++) obs[j] = r.obs[j];
-    const bool rs = live && (r.term || r.trunc) && p.auto_reset;
-    float u16[16];
-    reset_words_wave(p, rl, uint32_t(i), ep, rs, u16);
-    if (rs) {
-      if (out.terminal_obs) store_row12(out.terminal_obs, row, r.obs);
-      float init12[12], tgt[3], s12[12];
-      reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
-      env_reset_from<float, KIND>(K, e, init12, tgt, obs, s12);
-      ep += 1u;
-    }
-    store_obs_rows(lds, obs, out.obs + size_t(t) * size_t(n) * 12, block_first, n);
-    __syncthreads();  // the next step reuses the LDS rows
-  }
-  if (live) {
-    store_env(p, i, e, CTBR);
-    S.stu(F_EP, vo, ep);
-  }
-}
-
+// -- as ONE launch: `steps` whole steps per env with the action of step s drawn in-kernel from
+// quad_random_actions' map, Philox(seed; gid, step0 + s, 0x100), and the env state kept in registers
+// between steps (read once, written once). Per step every output row goes to HBM as in k_step_h:
+// obs [N,12], reward, flags, terminal obs of finishing envs, all time-major [steps][N, ...].
 // RB = envs per k_step_random_h block: 64 up to H_SMALL envs (4,096 envs: 2.22 vs 2.40 us per
 // step with 256), 256 above (65,536: 3.4 vs 4.5 us with 64); profiles/r02/ab_step_h_block.txt.
-// The same with helper waves (see k_step_h): a 512-thread block owns 256 envs; waves 0-3 step them,
+// The helper-wave form (see k_step_h): a 512-thread block owns 256 envs; waves 0-3 step them,
 // waves 4-7 draw -- two steps ahead -- each env's actions (quad_random_actions' Philox map) into a
 // double-buffered LDS slot, and keep each env's next-reset row (k_step_h's image) current: after
 // every step they read which envs reset, advance those episode counters and redraw their rows.
 // Per step: barrier A (flags known; the image is current) -> resets copied, obs rows staged ->
-// barrier B -> obs rows stored by all 512 threads, helpers redraw. Same bits as k_step_random.
+// barrier B -> obs rows stored by all 512 threads, helpers redraw. Same env_step code as k_step_h, so
+// the same bits as K single steps.
 template <int KIND, bool CTBR, int RB>
 __device__ __forceinline__ void helper_reset_row(const KConsts<float>& K, const KParams& p, int i, uint32_t ep,
                                                  float* H, int l) {
@@ -839,21 +636,6 @@ __global__ __launch_bounds__(2 * RB) void k_step_random_h(const KConsts<float>* 
   }
 }
 
-template <int KIND, bool CTBR, bool SPEC>
-__global__ __launch_bounds__(BLOCK) void k_step_random(const KConsts<float>* __restrict__ kc, KParams p,
-                                                       QuadStepOut out, float4* __restrict__ act_out,
-                                                       uint32_t step0, int32_t steps) {
-  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
-  __shared__ float4 lds[BLOCK * 3];
-  __shared__ ResetLds rl;
-  if constexpr (SPEC) {
-    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
-    step_random_body<KIND, CTBR>(K, p, out, act_out, step0, steps, lds, rl);
-  } else {
-    step_random_body<KIND, CTBR>(*kc, p, out, act_out, step0, steps, lds, rl);
-  }
-}
-
 // RelPosActWrapper (envs/wrappers.py:13-25) around HoverEnv / TrajectoryFollowEnv: the same step,
 // emitting obs7 = [obs[0:3], _prev_action] where _prev_action is the action just taken
 // (hover_env.py:166) and zeros after a reset (:212). The previous action is kept in the SoA
@@ -909,464 +691,6 @@ __global__ __launch_bounds__(BLOCK) void k_step_relpos(const KConsts<float>* __r
   for (int j = 0; j < 4; j++) S.st(F_PREV + j, vo, prev[j]);
 #pragma unroll
   for (int j = 0; j < 7; j++) out.obs[size_t(i) * 7 + j] = o7[j];
-}
-
-// ---------------------------------------------------------------------------------------------
-// k_step_g<KIND, CTBR, G>: the step with one env per GROUP of G lanes (G = 1, 2, 4; 64/G envs
-// per wave). Work that is a loop over 4 items in the one-thread form -- the props (hinge state and
-// inertia-box drag), the three atan2 of scipy's Euler algorithm, the four obs triples, the four
-// Philox blocks of the reset draw, the three half-angle sincos of from_euler -- is spread over the
-// group (lane l takes items l, l+G, ...); the rest is evaluated by every lane of the group (one
-// wave-instruction either way). Group reductions / broadcasts are DPP quad_perm (quad_lanes.h).
-// Why: at 65,536 envs the G = 1 form is one lone wave per SIMD (issue-latency bound); G > 1 buys
-// waves per SIMD at the price of the replicated part -- see DESIGN.md "Lane groups".
-template <int G, typename T>
-__device__ __forceinline__ T grp_pick(int m, const T* v) {  // v[m], m lane-dependent, m < 4
-  return pick4(m, v[0], v[1], v[2], v[3]);
-}
-
-template <int KIND, bool CTBR, int G>
-__device__ __forceinline__ void step_g_body(const KConsts<float>& k, KParams p, const float4* __restrict__ act,
-                                            QuadStepOut out) {
-  constexpr int NI = 4 / G;  // items per lane
-  const unsigned i_raw = unsigned(p.first) + (blockIdx.x * BLOCK + threadIdx.x) / G;
-  const int l = G == 1 ? 0 : int(threadIdx.x & (G - 1));
-  // G > 1: whole groups leave together. G = 1 keeps every thread (the LDS obs stage has a
-  // block barrier); out-of-range threads recompute the last env and store nothing.
-  const unsigned end = unsigned(p.first + p.count);
-  if (G > 1 && i_raw >= end) return;
-  const bool live = i_raw < end;
-  const unsigned i = live ? i_raw : end - 1;
-  const PhysConsts<float>& c = k.ph;
-  const Tiles S(p);
-  const uint32_t vo = env_off(i);
-  // ---- load: shared fields by every lane; per-prop / per-axis fields by their owner lane
-  float pos[3], q[4], v[3], w[3], tgt[3];
-#pragma unroll
-  for (int j = 0; j < 3; j++) {
-    pos[j] = S.ld(F_QPOS + j, vo);
-    v[j] = S.ld(F_QVEL + j, vo);
-    w[j] = S.ld(F_QVEL + 3 + j, vo);
-    tgt[j] = S.ld(F_TGT + j, vo);
-  }
-#pragma unroll
-  for (int j = 0; j < 4; j++) q[j] = S.ld(F_QPOS + 3 + j, vo);
-  float volt = S.ld(F_VOLT, vo);
-  int step = int(S.ldu(F_STEP, vo));
-  const uint32_t ep = S.ldu(F_EP, vo);  // prefetched: the reset branch must not add a dependent load
-  float th[NI], sp[NI];
-#pragma unroll
-  for (int it = 0; it < NI; it++) {
-    const int pr = l + it * G;
-    th[it] = G == 1 ? S.ld(F_QPOS + 7 + pr, vo) : S.ldv(F_QPOS + 7 + pr, vo);
-    sp[it] = G == 1 ? S.ld(F_QVEL + 6 + pr, vo) : S.ldv(F_QVEL + 6 + pr, vo);
-  }
-  float ri[3] = {0.f, 0.f, 0.f};
-  if (CTBR) {
-#pragma unroll
-    for (int j = 0; j < 3; j++) ri[j] = S.ld(F_RINT + j, vo);
-  }
-  const float4 a4 = act[i];
-  float a[4] = {a4.x, a4.y, a4.z, a4.w};
-
-  // ---- RateControlWrapper.action (float64): three axes, every lane (cheap, no reduction)
-  if (CTBR) {
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      const double err = double(a[1 + j]) * k.rate_max - double(w[j]);
-      const double rid = clipn(double(ri[j]) + k.rate_kidt * err, -k.rate_imax, k.rate_imax);
-      ri[j] = float(rid);
-      a[1 + j] = float(clipn((k.rate_ikd[j] * err + rid) * k.r_max_torque, -1.0, 1.0));
-    }
-  }
-  // ---- denormalize (float32) -> mixer, voltage sag, motor wrench (float64)
-  double phys[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) phys[j] = double(denorm1(a[j], k.act_lo[j], k.act_span[j]));
-  double F[4];
-#pragma unroll
-  for (int r = 0; r < 4; r++)
-    F[r] = clipn(c.mix[4 * r] * phys[0] + c.mix[4 * r + 1] * phys[1] + c.mix[4 * r + 2] * phys[2] +
-                     c.mix[4 * r + 3] * phys[3], 0.0, k.max_thrust);
-  const double vs = clipn(double(volt) * k.r_vnom, 0.0, 1.0);
-#pragma unroll
-  for (int r = 0; r < 4; r++) F[r] = clipn(F[r] * vs, 0.0, k.max_thrust * vs);
-  volt = float(clipn(double(volt) - (k.vb + k.vl * (((F[0] + F[1] + F[2] + F[3]) * 0.25) * k.r_mx)) * k.dt,
-                     k.vmin, k.vnom));
-  // ---- mujoco.mj_step: mj_checkPos/Vel, bad ctrl
-  int bad = 0;
-#pragma unroll
-  for (int it = 0; it < NI; it++) bad |= int(isbad(th[it])) | int(isbad(sp[it]));
-#pragma unroll
-  for (int j = 0; j < 3; j++) bad |= int(isbad(pos[j])) | int(isbad(v[j])) | int(isbad(w[j]));
-#pragma unroll
-  for (int j = 0; j < 4; j++) bad |= int(isbad(q[j]));
-  bad = group_or<G>(bad);
-  int badctrl = bad;
-#pragma unroll
-  for (int r = 0; r < 4; r++) badctrl |= int(isbad(F[r]));
-  if (bad) {
-#pragma unroll
-    for (int j = 0; j < 3; j++) { pos[j] = 0.f; v[j] = 0.f; w[j] = 0.f; }
-    q[0] = 1.f; q[1] = q[2] = q[3] = 0.f;
-#pragma unroll
-    for (int it = 0; it < NI; it++) { th[it] = 0.f; sp[it] = 0.f; }
-  }
-  double Fc[4];
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const double f = badctrl ? 0.0 : F[r];
-    Fc[r] = f < c.ctrl_lo ? c.ctrl_lo : (f > c.ctrl_hi ? c.ctrl_hi : f);
-  }
-  // ---- forward dynamics (forward_acc in quad_physics.h, props spread over the group)
-  float qn[4] = {q[0], q[1], q[2], q[3]};
-  normalize4(qn);
-  float R[9];
-  {
-    const float qw = qn[0], qx = qn[1], qy = qn[2], qz = qn[3];
-    R[0] = 1.f - 2.f * (qy * qy + qz * qz); R[1] = 2.f * (qx * qy - qw * qz); R[2] = 2.f * (qx * qz + qw * qy);
-    R[3] = 2.f * (qx * qy + qw * qz); R[4] = 1.f - 2.f * (qx * qx + qz * qz); R[5] = 2.f * (qy * qz - qw * qx);
-    R[6] = 2.f * (qx * qz - qw * qy); R[7] = 2.f * (qy * qz + qw * qx); R[8] = 1.f - 2.f * (qx * qx + qy * qy);
-  }
-  float vB[3];
-#pragma unroll
-  for (int j = 0; j < 3; j++) vB[j] = R[j] * v[0] + R[3 + j] * v[1] + R[6 + j] * v[2];
-  float FB[3] = {0.f, 0.f, 0.f}, tau[3] = {0.f, 0.f, 0.f}, Qs[NI], Qloc = 0.f, sloc = 0.f;
-#pragma unroll
-  for (int it = 0; it < NI; it++) {
-    const int pr = l + it * G;
-    const float pc[3] = {G == 1 ? c.pc[it][0] : pick4(pr, c.pc[0][0], c.pc[1][0], c.pc[2][0], c.pc[3][0]),
-                         G == 1 ? c.pc[it][1] : pick4(pr, c.pc[0][1], c.pc[1][1], c.pc[2][1], c.pc[3][1]),
-                         G == 1 ? c.pc[it][2] : pick4(pr, c.pc[0][2], c.pc[1][2], c.pc[2][2], c.pc[3][2])};
-    float sn, cs;
-    q_sincos(th[it], &sn, &cs);
-    float wxc[3];
-    cross(w, pc, wxc);
-    const float ub[3] = {vB[0] + wxc[0], vB[1] + wxc[1], vB[2] + wxc[2]};
-    const float wp[3] = {cs * w[0] + sn * w[1], -sn * w[0] + cs * w[1], w[2] + sp[it]};
-    const float up[3] = {cs * ub[0] + sn * ub[1], -sn * ub[0] + cs * ub[1], ub[2]};
-    float tp[3], fp[3];
-    box_drag(wp, up, c.p_kqa, c.p_kva, c.p_kql, c.p_kvl, tp, fp);
-    const float f[3] = {cs * fp[0] - sn * fp[1], sn * fp[0] + cs * fp[1], fp[2]};
-    const float t[3] = {cs * tp[0] - sn * tp[1], sn * tp[0] + cs * tp[1], tp[2]};
-    float rxf[3];
-    cross(pc, f, rxf);
-#pragma unroll
-    for (int j = 0; j < 3; j++) { FB[j] += f[j]; tau[j] += rxf[j] + t[j]; }
-    Qs[it] = tp[2];
-    Qloc += tp[2];
-    sloc += sp[it];
-  }
-#pragma unroll
-  for (int j = 0; j < 3; j++) { FB[j] = group_sum<G>(FB[j]); tau[j] = group_sum<G>(tau[j]); }
-  const float Qsum = group_sum<G>(Qloc), ssum = group_sum<G>(sloc);
-  {  // motor wrench (float64 -> float32), gravity at the system COM, base inertia-box drag
-    FB[2] += float(Fc[0] + Fc[1] + Fc[2] + Fc[3]);
-    tau[0] += float(c.syd[0] * Fc[0] + c.syd[1] * Fc[1] + c.syd[2] * Fc[2] + c.syd[3] * Fc[3]);
-    tau[1] += float(-(c.sxd[0] * Fc[0] + c.sxd[1] * Fc[1] + c.sxd[2] * Fc[2] + c.sxd[3] * Fc[3]));
-    tau[2] += float(c.g5d[0] * Fc[0] + c.g5d[1] * Fc[1] + c.g5d[2] * Fc[2] + c.g5d[3] * Fc[3]);
-    const float mg = c.mt * c.gz;
-    const float gB[3] = {mg * R[6], mg * R[7], mg * R[8]};
-    float tg[3];
-    cross(c.cbar, gB, tg);
-    float tb[3], fb[3];
-    box_drag(w, vB, c.b_kqa, c.b_kva, c.b_kql, c.b_kvl, tb, fb);
-#pragma unroll
-    for (int j = 0; j < 3; j++) { FB[j] += gB[j] + fb[j]; tau[j] += tg[j] + tb[j]; }
-  }
-  float vdot[3], wdot[3], sdot[NI];
-  {
-    float wc[3], wwc[3], fv[3], Iw[3], wIw[3], cxf[3], rhs[3], cxw[3], aB[3];
-    cross(w, c.cbar, wc);
-    cross(w, wc, wwc);
-#pragma unroll
-    for (int j = 0; j < 3; j++) fv[j] = FB[j] - c.mt * wwc[j];
-#pragma unroll
-    for (int j = 0; j < 3; j++) Iw[j] = c.IO[3 * j] * w[0] + c.IO[3 * j + 1] * w[1] + c.IO[3 * j + 2] * w[2];
-    cross(w, Iw, wIw);
-    cross(c.cbar, fv, cxf);
-    rhs[0] = tau[0] - wIw[0] - c.c_ax * ssum * w[1] - cxf[0];
-    rhs[1] = tau[1] - wIw[1] + c.c_ax * ssum * w[0] - cxf[1];
-    rhs[2] = tau[2] - wIw[2] - Qsum - cxf[2];
-#pragma unroll
-    for (int j = 0; j < 3; j++) wdot[j] = c.Ainv[3 * j] * rhs[0] + c.Ainv[3 * j + 1] * rhs[1] + c.Ainv[3 * j + 2] * rhs[2];
-    cross(c.cbar, wdot, cxw);
-#pragma unroll
-    for (int j = 0; j < 3; j++) aB[j] = fv[j] * c.inv_mt + cxw[j];
-#pragma unroll
-    for (int j = 0; j < 3; j++) vdot[j] = R[3 * j] * aB[0] + R[3 * j + 1] * aB[1] + R[3 * j + 2] * aB[2];
-#pragma unroll
-    for (int it = 0; it < NI; it++) sdot[it] = Qs[it] * c.inv_c_ax - wdot[2];
-  }
-  {  // mj_checkAcc: reset to qpos0; at rest there qacc is free fall
-    int badacc = 0;
-#pragma unroll
-    for (int it = 0; it < NI; it++) badacc |= int(isbad(sdot[it]));
-#pragma unroll
-    for (int j = 0; j < 3; j++) badacc |= int(isbad(vdot[j])) | int(isbad(wdot[j]));
-    if (group_or<G>(badacc)) {
-#pragma unroll
-      for (int j = 0; j < 3; j++) { pos[j] = 0.f; v[j] = 0.f; w[j] = 0.f; vdot[j] = 0.f; wdot[j] = 0.f; }
-      vdot[2] = c.gz;
-      qn[0] = 1.f; qn[1] = qn[2] = qn[3] = 0.f;
-#pragma unroll
-      for (int it = 0; it < NI; it++) { th[it] = 0.f; sp[it] = 0.f; sdot[it] = 0.f; }
-    }
-  }
-  // ---- mj_Euler: semi-implicit update, MuJoCo quaternion integration
-  const float h = c.dt;
-#pragma unroll
-  for (int j = 0; j < 3; j++) {
-    v[j] += h * vdot[j];
-    w[j] += h * wdot[j];
-    pos[j] += h * v[j];
-  }
-#pragma unroll
-  for (int it = 0; it < NI; it++) {
-    sp[it] += h * sdot[it];
-    th[it] += h * sp[it];
-  }
-  {
-    const float w2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
-    const float x2 = 0.25f * h * h * w2;
-    float qr[4];
-    if (x2 < 0.0625f) {
-      const float ch = 1.f + x2 * (-0.5f + x2 * (1.f / 24 + x2 * (-1.f / 720 + x2 * (1.f / 40320))));
-      const float sc = 1.f + x2 * (-1.f / 6 + x2 * (1.f / 120 + x2 * (-1.f / 5040 + x2 * (1.f / 362880))));
-      const float kk = 0.5f * h * sc;
-      qr[0] = ch; qr[1] = w[0] * kk; qr[2] = w[1] * kk; qr[3] = w[2] * kk;
-    } else {
-      const float wn = fsqrt(w2);
-      float sh, chh;
-      q_sincos(0.5f * h * wn, &sh, &chh);
-      const float kk = sh / wn;
-      qr[0] = chh; qr[1] = w[0] * kk; qr[2] = w[1] * kk; qr[3] = w[2] * kk;
-    }
-    q[0] = qn[0] * qr[0] - qn[1] * qr[1] - qn[2] * qr[2] - qn[3] * qr[3];
-    q[1] = qn[0] * qr[1] + qn[1] * qr[0] + qn[2] * qr[3] - qn[3] * qr[2];
-    q[2] = qn[0] * qr[2] - qn[1] * qr[3] + qn[2] * qr[0] + qn[3] * qr[1];
-    q[3] = qn[0] * qr[3] + qn[1] * qr[2] - qn[2] * qr[1] + qn[3] * qr[0];
-  }
-  step += 1;
-  // ---- QuadState (scipy as_euler('xyz')): items 0,1,2 = mid, half_sum, half_diff atan2
-  float s12[12];
-  {
-    const float inv = frsqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-    const float qw = q[0] * inv, qx = q[1] * inv, qy = q[2] * inv, qz = q[3] * inv;
-    const float A = qw - qy, B = qx + qz, Cc = qy + qw, D = qz - qx;
-    const float ys[4] = {q_hypot(Cc, D), B, D, D};
-    const float xs[4] = {q_hypot(A, B), A, Cc, Cc};
-    float at[3];
-    if constexpr (G == 1) {
-#pragma unroll
-      for (int m = 0; m < 3; m++) at[m] = q_atan2(ys[m], xs[m]);
-    } else if constexpr (G == 2) {
-      const float r0 = q_atan2(l ? ys[1] : ys[0], l ? xs[1] : xs[0]);  // items 0 | 1
-      const float r1 = q_atan2(ys[2], xs[2]);                           // item 2 (both lanes)
-      at[0] = group_bc<G, 0>(r0); at[1] = group_bc<G, 1>(r0); at[2] = r1;
-    } else {
-      const float r = q_atan2(grp_pick<G>(l, ys), grp_pick<G>(l, xs));
-      at[0] = group_bc<G, 0>(r); at[1] = group_bc<G, 1>(r); at[2] = group_bc<G, 2>(r);
-    }
-    const float PI = 3.14159265358979323846f;
-    const float mid = 2.f * at[0], hs = at[1], hd = at[2];
-    const bool case1 = fabsf(mid) <= 1e-7f, case2 = fabsf(mid - PI) <= 1e-7f;
-    float e[3];
-    if (!(case1 || case2)) { e[0] = hs - hd; e[2] = hs + hd; }
-    else { e[2] = 0.f; e[0] = case1 ? 2.f * hs : -2.f * hd; }
-    e[1] = mid - PI / 2.f;
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      if (e[j] < -PI) e[j] += 2.f * PI;
-      else if (e[j] > PI) e[j] -= 2.f * PI;
-    }
-#pragma unroll
-    for (int j = 0; j < 3; j++) { s12[j] = pos[j]; s12[3 + j] = e[j]; s12[6 + j] = v[j]; s12[9 + j] = w[j]; }
-  }
-  const float reward = reward_of<float>(s12, tgt);
-  const bool term = terminated_of(k, s12);
-  const bool trunc = step >= k.max_steps;
-  // obs triples m = l + it*G (normalize, float32, correctly rounded)
-  float ob[NI][3];
-  auto obs_triples = [&](const float* st, const float* tg3) {
-#pragma unroll
-    for (int it = 0; it < NI; it++) {
-      const int m = l + it * G;
-#pragma unroll
-      for (int j = 0; j < 3; j++) {
-        float x, lo, sp_, rs;
-        if constexpr (G == 1) {
-          x = st[3 * it + j]; lo = k.obs_lo[3 * it + j]; sp_ = k.obs_span[3 * it + j]; rs = k.obs_rspan[3 * it + j];
-        } else {
-          x = pick4(m, st[j], st[3 + j], st[6 + j], st[9 + j]);
-          lo = pick4(m, k.obs_lo[j], k.obs_lo[3 + j], k.obs_lo[6 + j], k.obs_lo[9 + j]);
-          sp_ = pick4(m, k.obs_span[j], k.obs_span[3 + j], k.obs_span[6 + j], k.obs_span[9 + j]);
-          rs = pick4(m, k.obs_rspan[j], k.obs_rspan[3 + j], k.obs_rspan[6 + j], k.obs_rspan[9 + j]);
-        }
-        if (m == 0) x = sub32(tg3[j], x);
-        ob[it][j] = norm_obs1(x, lo, sp_, rs);
-      }
-    }
-  };
-  obs_triples(s12, tgt);
-  settle(ep);
-  if (l == 0 && live) {
-    out.reward[i] = reward;
-    out.terminated[i] = term;
-    out.truncated[i] = trunc;
-    if (out.voltage_scale) out.voltage_scale[i] = float(vs);
-    if (out.motor_commands)
-      reinterpret_cast<float4*>(out.motor_commands)[i] = make_float4(float(F[0]), float(F[1]), float(F[2]), float(F[3]));
-  }
-  if (G == 1 && out.state12 && live) {
-    store_row12(out.state12, i, s12);
-  } else if (out.state12 && live) {
-#pragma unroll
-    for (int it = 0; it < NI; it++) {
-      const int m = l + it * G;
-#pragma unroll
-      for (int j = 0; j < 3; j++)
-        out.state12[size_t(i) * 12 + 3 * m + j] = G == 1 ? s12[3 * it + j] : pick4(m, s12[j], s12[3 + j], s12[6 + j], s12[9 + j]);
-    }
-  }
-  if (out.target_info && live && l == 0) {  // info target (+ spline velocity / acceleration)
-    float o[9] = {tgt[0], tgt[1], tgt[2], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (KIND == QUAD_ENV_TRAJ) traj_spline_info(k, p.seed, p.gid_base + uint64_t(i), ep - 1u, tgt, step, o);
-#pragma unroll
-    for (int j = 0; j < 9; j++) out.target_info[size_t(i) * 9 + j] = o[j];
-  }
-  // ---- SB3 auto-reset (group-uniform branch)
-  const bool reset = (term || trunc) && p.auto_reset;
-  if (reset) {
-    if (out.terminal_obs && live) {
-      if constexpr (G == 1) {
-        const float o12[12] = {ob[0][0], ob[0][1], ob[0][2], ob[1][0], ob[1][1], ob[1][2],
-                               ob[2][0], ob[2][1], ob[2][2], ob[3][0], ob[3][1], ob[3][2]};
-        store_row12(out.terminal_obs, i, o12);
-      } else {
-#pragma unroll
-        for (int it = 0; it < NI; it++)
-#pragma unroll
-          for (int j = 0; j < 3; j++) out.terminal_obs[size_t(i) * 12 + 3 * (l + it * G) + j] = ob[it][j];
-      }
-    }
-    const uint64_t gid = p.gid_base + uint64_t(i);
-    uint32_t r[NI][4];
-#pragma unroll
-    for (int it = 0; it < NI; it++) {  // Philox blocks l, l+G, ...
-      r[it][0] = uint32_t(gid); r[it][1] = uint32_t(gid >> 32); r[it][2] = ep; r[it][3] = uint32_t(l + it * G);
-      philox4x32_10(r[it], uint32_t(p.seed), uint32_t(p.seed >> 32));
-    }
-    uint32_t wd[15];  // word j of the 16-word draw lives in block j/4 -> lane (j/4)%G, item (j/4)/G
-#define QD_W(J) wd[J] = group_bcu<G, ((J) / 4) % G>(r[((J) / 4) / G][(J) % 4]);
-    QD_W(0) QD_W(1) QD_W(2) QD_W(3) QD_W(4) QD_W(5) QD_W(6) QD_W(7)
-    QD_W(8) QD_W(9) QD_W(10) QD_W(11) QD_W(12) QD_W(13) QD_W(14)
-#undef QD_W
-    float init12[12], tg[3];
-#pragma unroll
-    for (int j = 0; j < 12; j++) init12[j] = affine32(k.init_lo[j], u01(wd[j]), k.init_span[j]);
-#pragma unroll
-    for (int j = 0; j < 3; j++) tg[j] = affine32(k.tgt_lo[j], u01(wd[12 + j]), k.tgt_span[j]);
-    // from_euler: half-angle sincos of axes 0..2 spread over the group
-    float hsn[3], hcs[3];
-    if constexpr (G == 1) {
-#pragma unroll
-      for (int m = 0; m < 3; m++) q_sincos(init12[3 + m] * 0.5f, &hsn[m], &hcs[m]);
-    } else if constexpr (G == 2) {
-      float s0, c0;
-      q_sincos((l ? init12[4] : init12[3]) * 0.5f, &s0, &c0);
-      q_sincos(init12[5] * 0.5f, &hsn[2], &hcs[2]);
-      hsn[0] = group_bc<G, 0>(s0); hcs[0] = group_bc<G, 0>(c0);
-      hsn[1] = group_bc<G, 1>(s0); hcs[1] = group_bc<G, 1>(c0);
-    } else {
-      float s0, c0;
-      q_sincos(pick4(l, init12[3], init12[4], init12[5], init12[5]) * 0.5f, &s0, &c0);
-      hsn[0] = group_bc<G, 0>(s0); hcs[0] = group_bc<G, 0>(c0);
-      hsn[1] = group_bc<G, 1>(s0); hcs[1] = group_bc<G, 1>(c0);
-      hsn[2] = group_bc<G, 2>(s0); hcs[2] = group_bc<G, 2>(c0);
-    }
-    {
-      const float sr = hsn[0], cr = hcs[0], spp = hsn[1], cp = hcs[1], sy = hsn[2], cy = hcs[2];
-      q[0] = cy * cp * cr + sy * spp * sr;
-      q[1] = cy * cp * sr - sy * spp * cr;
-      q[2] = cy * spp * cr + sy * cp * sr;
-      q[3] = sy * cp * cr - cy * spp * sr;
-    }
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      pos[j] = init12[j];
-      v[j] = init12[6 + j];
-      w[j] = init12[9 + j];
-      tgt[j] = KIND == QUAD_ENV_TRAJ ? init12[j] : tg[j];
-      ri[j] = 0.f;
-    }
-#pragma unroll
-    for (int it = 0; it < NI; it++) { th[it] = 0.f; sp[it] = 0.f; }
-    volt = float(k.vnom);
-    step = 0;
-    obs_triples(init12, tgt);  // QuadState round trip of the drawn state == the draw itself
-    if (l == 0 && live) S.stu(F_EP, vo, ep + 1u);
-  }
-  // ---- stores: obs rows. G = 1: staged through LDS so every wave-store writes 1 KiB
-  // contiguously; G > 1: one dwordx3 per lane, a wave's rows are already contiguous.
-  if constexpr (G == 1) {
-    __shared__ float4 lds[BLOCK * 3];
-    const float o12[12] = {ob[0][0], ob[0][1], ob[0][2], ob[1][0], ob[1][1], ob[1][2],
-                           ob[2][0], ob[2][1], ob[2][2], ob[3][0], ob[3][1], ob[3][2]};
-    store_obs_rows(lds, o12, out.obs, p.first + int(blockIdx.x) * BLOCK, int(end));
-  } else {
-#pragma unroll
-    for (int it = 0; it < NI; it++) {
-      float* o = out.obs + size_t(i) * 12 + 3 * (l + it * G);
-      o[0] = ob[it][0]; o[1] = ob[it][1]; o[2] = ob[it][2];
-    }
-  }
-  if (!live) return;
-#pragma unroll
-  for (int it = 0; it < NI; it++) {
-    const int pr = l + it * G;
-    if (G == 1) {
-      S.st(F_QPOS + 7 + pr, vo, th[it]);
-      S.st(F_QVEL + 6 + pr, vo, sp[it]);
-    } else {
-      S.stv(F_QPOS + 7 + pr, vo, th[it]);
-      S.stv(F_QVEL + 6 + pr, vo, sp[it]);
-    }
-  }
-  if (l == 0) {
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      S.st(F_QPOS + j, vo, pos[j]);
-      S.st(F_QVEL + j, vo, v[j]);
-      S.st(F_QVEL + 3 + j, vo, w[j]);
-      if (reset) S.st(F_TGT + j, vo, tgt[j]);  // the target only changes on reset
-      if (CTBR) S.st(F_RINT + j, vo, ri[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) S.st(F_QPOS + 3 + j, vo, q[j]);
-    S.st(F_VOLT, vo, volt);
-    S.stu(F_STEP, vo, uint32_t(step));
-  }
-}
-
-// QD_G_WAVES (A/B builds of tools/probe/build_variant.sh only): a minimum waves-per-SIMD target
-#if defined(QD_G_WAVES)
-#define QD_G_ATTR __attribute__((amdgpu_waves_per_eu(QD_G_WAVES, 8)))
-#else
-#define QD_G_ATTR
-#endif
-template <int KIND, bool CTBR, int G, bool SPEC>
-__global__ __launch_bounds__(BLOCK) QD_G_ATTR void k_step_g(float* tiles, const float4* __restrict__ act, uint32_t tile_bytes,
-                                                  int32_t first, int32_t count, const KConsts<float>* __restrict__ kc,
-                                                  KParams p, QuadStepOut out) {
-  p.tiles = tiles; p.tile_bytes = tile_bytes; p.first = first; p.count = count;  // preloaded (see k_step)
-  p.kc = kc;  // noalias: constant-block loads stay scalar after the stores (see KParams)
-  if constexpr (SPEC) {
-    constexpr KConsts<float> K = kdef_block<KIND, CTBR>();
-    step_g_body<KIND, CTBR, G>(K, p, act, out);
-  } else {
-    step_g_body<KIND, CTBR, G>(*kc, p, act, out);
-  }
 }
 
 template <int KIND, bool RELPOS>
@@ -1655,7 +979,6 @@ __global__ __launch_bounds__(BLOCK) void k_gae(const float* __restrict__ rew, co
 
 struct QuadHandle {
   QuadCfg cfg;
-  int lanes = 1;  // lanes per env in k_step_g (1, 2, 4); 0 = k_step. QUADENV_LANES overrides
   PhysConstsD pd;
   KParams kp;
   int device;
@@ -1665,8 +988,7 @@ struct QuadHandle {
   uint32_t* stage = nullptr;  // [NFT][n] staging for host-side get/set_state, allocated on first use
   KConsts<float> kh;                 // host copy of the constant block
   KConsts<float>* kdev = nullptr;    // device copy the kernels read (scalar loads, K$-resident)
-  bool spec = false;                 // kh == a reference default block: k_step's SPEC form
-  bool helper = true;                // one-thread form: k_step_h (helper waves draw the resets)
+  bool spec = false;                 // kh == a reference default block: k_step_h's SPEC form
   int hblock = 0;                    // envs per k_step_h block: 0 = by size (h_wide: 256 between H_SMALL and 2M, else 64)
   int hd = -1;                       // k_step_hd for the 64-env nt launches: -1 = by size (hd_form), 0 / 1
   int nt = -1;                       // k_step_h's state cache policy: -1 = by size (nt_state), 0 / 1
@@ -1765,9 +1087,6 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   make_kconsts<float>(*cfg, h->pd, h->kh);
   h->spec = is_default_block(h->kh, cfg->env_kind, cfg->wrapper == QUAD_WRAP_CTBR);
   if (const char* v = std::getenv("QUADENV_SPEC")) h->spec = h->spec && std::atoi(v) != 0;
-  // measured: helper waves 6.54 -> 5.87 us at 65,536 envs, 5.74 -> 4.24 at 4,096;
-  // QUADENV_HELPER=0 keeps the plain k_step (A/B and tests)
-  if (const char* v = std::getenv("QUADENV_HELPER")) h->helper = std::atoi(v) != 0;
   // QUADENV_HBLOCK=64|256 pins the helper form's block size (tests run the 256-env blocks at small N)
   if (const char* v = std::getenv("QUADENV_NT")) h->nt = std::atoi(v) != 0 ? 1 : 0;
   if (const char* v = std::getenv("QUADENV_HD")) h->hd = std::atoi(v) != 0 ? 1 : 0;
@@ -1797,16 +1116,12 @@ int quad_create(const QuadCfg* cfg, int32_t device, uint64_t seed, uint64_t env_
   h->kp.auto_reset = cfg->auto_reset;
   h->kp.seed = seed;
   h->kp.gid_base = env_id_base;
-  // measured on MI355X (round 4, tools/step_env_ab.py, profiles/r04/r4_step_forms_nt.txt and
-  // r4_step_nt_sizes.txt): the helper-wave form k_step_h (256-env blocks above 32,768 envs) with
-  // its size-chosen cache policy (nt_state) is the fastest form at every size -- 262,144 envs 14.4
-  // vs 15.9 us for k_step_g<1>, 1M 51.1 vs 51.9, 2M 97 vs 117 for k_step_g<2> (both nt), 4M 268.6 vs
-  // 268.3, 8M 546 vs 557; the lane-group forms k_step_g<G> stay selectable (QUADENV_LANES)
-  h->lanes = 0;
-  if (const char* v = std::getenv("QUADENV_LANES")) {
-    const int g = std::atoi(v);
-    if (g == 0 || g == 1 || g == 2 || g == 4) h->lanes = g;
-  }
+  // The step forms: the helper-wave form k_step_h (256-env blocks above 32,768 envs) with
+  // its size-chosen cache policy (nt_state) and k_step_hd from 4M envs measured fastest at every size
+  // (round 2: helper waves 6.54 -> 5.87 us at 65,536 envs, 5.74 -> 4.24 at 4,096 against the one-wave
+  // form; round 4, profiles/r04/r4_step_forms_nt.txt and r4_step_nt_sizes.txt: 262,144 envs 14.4 vs
+  // 15.9 us for the lane-group form with one env per lane, 1M 51.1 vs 51.9, 2M 97 vs 117 for two lanes
+  // per env). The one-wave and lane-group forms were A/B builds; round 6 removed them from the library.
   *out = h;
   return QUAD_OK;
 }
@@ -1827,10 +1142,9 @@ int32_t quad_kernel_form(const QuadHandle* h) {
   // RELPOS and the brax kinds have one kernel each (k_step_relpos / k_step_brax): no lanes, SPEC
   // or helper forms to report
   if (wrap_relpos(h->cfg.wrapper) || h->cfg.env_kind >= QUAD_ENV_BRAX_HOVER) return 64;
-  const bool wide = h_wide(h, h->n);
-  return h->lanes | (h->spec ? 16 : 0) | (h->lanes == 0 && h->helper ? 32 : 0) |
-         (h->lanes == 0 && h->helper && wide ? 128 : 0) | (h->lanes == 0 && h->helper && nt_state(h, h->n) ? 256 : 0) |
-         (h->lanes == 0 && h->helper && hd_form(h, h->n) ? 512 : 0);
+  // bit 5: the helper-wave form (always; bits 0-2 were the removed lane-group forms)
+  return (h->spec ? 16 : 0) | 32 | (h_wide(h, h->n) ? 128 : 0) | (nt_state(h, h->n) ? 256 : 0) |
+         (hd_form(h, h->n) ? 512 : 0);
 }
 
 int quad_seed(QuadHandle* h, uint64_t seed, void* stream) {
@@ -1884,7 +1198,6 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
   const float4* a = reinterpret_cast<const float4*>(actions);
   const bool traj = h->cfg.env_kind == QUAD_ENV_TRAJ, ctbr = h->cfg.wrapper == QUAD_WRAP_CTBR;
   const dim3 blk(BLOCK);
-  const int G = h->lanes;
   KParams kp = h->kp;
   kp.first = first;
   kp.count = count;
@@ -1905,18 +1218,8 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
       hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_TRAJ>), grid, blk, 0, s, h->kdev, kp, a, *out);
     else
       hipLaunchKernelGGL((k_step_brax<QUAD_ENV_BRAX_HOVER>), grid, blk, 0, s, h->kdev, kp, a, *out);
-  } else if (G == 0) {  // one thread per env with the LDS obs transpose
-    const dim3 grid(grid_of(count));
+  } else {  // one thread per env, helper waves beside the step waves
 #define QD_KARGS kp.tiles, a, kp.tile_bytes, kp.first, kp.count, h->kdev, kp, *out
-#define QD_LAUNCH_K(SP)                                                                            \
-  if (traj && ctbr)                                                                             \
-    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, true, SP>), grid, blk, 0, s, QD_KARGS);      \
-  else if (traj)                                                                                \
-    hipLaunchKernelGGL((k_step<QUAD_ENV_TRAJ, false, SP>), grid, blk, 0, s, QD_KARGS);     \
-  else if (ctbr)                                                                                \
-    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, QD_KARGS);     \
-  else                                                                                          \
-    hipLaunchKernelGGL((k_step<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, QD_KARGS);
 #define QD_LAUNCH_H2(SP, HB, NT)                                                                       \
   if (traj && ctbr)                                                                             \
     hipLaunchKernelGGL((k_step_h<QUAD_ENV_TRAJ, true, SP, HB, NT>), grid, blk2, 0, s, QD_KARGS);      \
@@ -1939,40 +1242,20 @@ int quad_step_range(QuadHandle* h, int32_t first, int32_t count, const float* ac
     hipLaunchKernelGGL((k_step_hd<QUAD_ENV_HOVER, false, SP>), grid, blk2, 0, s, QD_KARGS);
     const bool wide = h_wide(h, count);
     const bool nt = nt_state(h, count);
-    if (h->helper && hd_form(h, count)) {
+    if (hd_form(h, count)) {
       const dim3 grid(unsigned((int64_t(count) + 63) / 64)), blk2(128);
       if (h->spec) { QD_LAUNCH_HD(true) } else { QD_LAUNCH_HD(false) }
-    } else if (h->helper && !wide) {
+    } else if (!wide) {
       const dim3 grid(unsigned((int64_t(count) + 63) / 64)), blk2(128);
       if (h->spec) { QD_LAUNCH_H(true, 64) } else { QD_LAUNCH_H(false, 64) }
-    } else if (h->helper) {
+    } else {
       const dim3 grid(unsigned((int64_t(count) + 255) / 256)), blk2(512);
       if (h->spec) { QD_LAUNCH_H(true, 256) } else { QD_LAUNCH_H(false, 256) }
-    } else if (h->spec) { QD_LAUNCH_K(true) } else { QD_LAUNCH_K(false) }
-#undef QD_LAUNCH_K
+    }
 #undef QD_LAUNCH_H
 #undef QD_LAUNCH_H2
 #undef QD_LAUNCH_HD
 #undef QD_KARGS
-  } else {
-    const dim3 grid(unsigned((int64_t(count) * G + BLOCK - 1) / BLOCK));
-#define QD_GARGS kp.tiles, a, kp.tile_bytes, kp.first, kp.count, h->kdev, kp, *out
-#define QD_LAUNCH(GG, SP)                                                                          \
-  if (traj && ctbr)                                                                             \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, true, GG, SP>), grid, blk, 0, s, QD_GARGS);   \
-  else if (traj)                                                                                \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_TRAJ, false, GG, SP>), grid, blk, 0, s, QD_GARGS);  \
-  else if (ctbr)                                                                                \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, true, GG, SP>), grid, blk, 0, s, QD_GARGS);  \
-  else                                                                                          \
-    hipLaunchKernelGGL((k_step_g<QUAD_ENV_HOVER, false, GG, SP>), grid, blk, 0, s, QD_GARGS);
-    if (G == 1) {  // the batch-size default above 262,144 envs: SPEC form when the block is the default
-      if (h->spec) { QD_LAUNCH(1, true) } else { QD_LAUNCH(1, false) }
-    } else if (G == 2) {
-      if (h->spec) { QD_LAUNCH(2, true) } else { QD_LAUNCH(2, false) }
-    } else { QD_LAUNCH(4, false) }
-#undef QD_LAUNCH
-#undef QD_GARGS
   }
   HIP_TRY(hipGetLastError());
   return QUAD_OK;
@@ -2020,6 +1303,27 @@ int quad_observe(QuadHandle* h, float* obs, float* state12, void* stream) {
   return QUAD_OK;
 }
 
+int quad_mem_floor(QuadHandle* h, const float* actions, const QuadStepOut* out, void* stream) {
+  if (!h || !actions || !out) return fail(QUAD_EINVAL, "handle/actions/out is NULL");
+  if (!out->obs || !out->reward || !out->terminated || !out->truncated)
+    return fail(QUAD_EINVAL, "obs, reward, terminated and truncated are required");
+  if ((reinterpret_cast<uintptr_t>(actions) | reinterpret_cast<uintptr_t>(out->obs)) & 15u)
+    return fail(QUAD_EINVAL, "actions and obs must be 16-byte aligned");
+  if (h->cfg.env_kind != QUAD_ENV_HOVER && h->cfg.env_kind != QUAD_ENV_TRAJ)
+    return fail(QUAD_EINVAL, "quad_mem_floor: hover / trajectory kinds");
+  if (wrap_relpos(h->cfg.wrapper)) return fail(QUAD_EINVAL, "quad_mem_floor: no RELPOS (7-D obs rows)");
+  DeviceGuard g(h->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const dim3 grid(unsigned((int64_t(h->n) + 255) / 256)), blk(256);
+  const float4* a = reinterpret_cast<const float4*>(actions);
+  if (nt_state(h, h->n))
+    hipLaunchKernelGGL(k_mem_floor<2>, grid, blk, 0, s, h->kp, a, *out);
+  else
+    hipLaunchKernelGGL(k_mem_floor<0>, grid, blk, 0, s, h->kp, a, *out);
+  HIP_TRY(hipGetLastError());
+  return QUAD_OK;
+}
+
 int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadStepOut* out, float* actions_out,
                      void* stream) {
   if (!h || !out) return fail(QUAD_EINVAL, "handle/out is NULL");
@@ -2038,18 +1342,8 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
     return fail(QUAD_EINVAL, "steps * N too large for one launch (time-major rows use 32-bit byte offsets)");
   DeviceGuard g(h->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
-  const dim3 grid(grid_of(h->n)), blk(BLOCK);
   float4* ao = reinterpret_cast<float4*>(actions_out);
   const bool traj = h->cfg.env_kind == QUAD_ENV_TRAJ, ctbr = h->cfg.wrapper == QUAD_WRAP_CTBR;
-#define QD_LAUNCH_R(SP)                                                                                     \
-  if (traj && ctbr)                                                                                      \
-    hipLaunchKernelGGL((k_step_random<QUAD_ENV_TRAJ, true, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);   \
-  else if (traj)                                                                                         \
-    hipLaunchKernelGGL((k_step_random<QUAD_ENV_TRAJ, false, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
-  else if (ctbr)                                                                                         \
-    hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, true, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
-  else                                                                                                   \
-    hipLaunchKernelGGL((k_step_random<QUAD_ENV_HOVER, false, SP>), grid, blk, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
 #define QD_LAUNCH_RH(SP, RB)                                                                                     \
   if (traj && ctbr)                                                                                      \
     hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_TRAJ, true, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);   \
@@ -2062,14 +1356,13 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
   // the block size of k_step_h's policy (h_wide: 64-env blocks up to H_SMALL and from 2M envs);
   // the K-step form reads and writes its state once per launch, so the nt policy does not apply
   const bool wide = h_wide(h, h->n);
-  if (h->helper && !wide) {
+  if (!wide) {
     const dim3 grid(unsigned((int64_t(h->n) + 63) / 64)), blk2(128);
     if (h->spec) { QD_LAUNCH_RH(true, 64) } else { QD_LAUNCH_RH(false, 64) }
-  } else if (h->helper) {
+  } else {
     const dim3 grid(unsigned((int64_t(h->n) + 255) / 256)), blk2(512);
     if (h->spec) { QD_LAUNCH_RH(true, 256) } else { QD_LAUNCH_RH(false, 256) }
-  } else if (h->spec) { QD_LAUNCH_R(true) } else { QD_LAUNCH_R(false) }
-#undef QD_LAUNCH_R
+  }
 #undef QD_LAUNCH_RH
   HIP_TRY(hipGetLastError());
   return QUAD_OK;

@@ -106,11 +106,8 @@ __device__ __forceinline__ void store_row(float* __restrict__ base, size_t row, 
   b4[2] = make_float4(v[8], v[9], v[10], v[11]);
 }
 
-// QD_ROLL_ALP: the actor's W2 pieces from LDS (policy_net.h stage_pieces / LP_SPLIT), the
-// critic's from L2; 0 = both from L2 (round 3). Same bits.
-#ifndef QD_ROLL_ALP
-#define QD_ROLL_ALP 1
-#endif
+// The actor's W2 pieces come from LDS (policy_net.h stage_pieces / LP_SPLIT), the critic's from L2
+// (round 4; both from L2 was round 3's form, same bits).
 
 // the Gaussian action of this lane's env (SB3 policy.forward: a = mean + std z), its log-prob as
 // PPO.train recomputes it, and the clipped action the env receives
@@ -167,9 +164,7 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
   }
   float ls = a.last_start[i], ret = a.ep_ret[i], len = a.ep_len[i];
   stage_lds<BLK>(lds, packed);
-#if QD_ROLL_ALP
   stage_pieces<BLK>(lds, packed);  // the actor's W2 pieces, once per launch
-#endif
   const float* log_std = packed + LDS_F;
   float lstd[ACT], sd[ACT];
 #pragma unroll
@@ -196,7 +191,7 @@ __device__ __forceinline__ void rollout_body(const KConsts<float>& K, KParams p,
 #pragma unroll
     for (int j = 0; j < NT; j++) val[j][0] = mean[j][0];
 #else
-    net_forward2<NT, bool(QD_ROLL_ALP)>(lds, packed, xb, mean, val);
+    net_forward2<NT, true>(lds, packed, xb, mean, val);
 #endif
 #endif
     float act[ACT], ac[ACT], lp = 0.f;

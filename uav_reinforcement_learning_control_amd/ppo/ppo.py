@@ -381,14 +381,14 @@ class PPO:
         local = self._done_stats.clone()
         if self.world > 1:
             dist.all_reduce(self._done_stats, op=dist.ReduceOp.SUM)
-        torch.cuda.synchronize(self.device)
+        # one host read of the reduced sums and this rank's count (the synchronize of the copy)
+        ret_sum, len_sum, c, local_c = torch.cat([self._done_stats, local[2:]]).tolist()
         steps = self.cfg.n_steps * self.env.num_envs
         self.num_timesteps += steps * self.world
-        ret_sum, len_sum, c = self._done_stats.tolist()
         return RolloutStats(episodes=int(c), mean_return=ret_sum / c if c else float("nan"),
                             mean_length=len_sum / c if c else float("nan"),
                             env_steps=steps, seconds=time.perf_counter() - t0,
-                            extra={"local_episodes": int(local[2].item()), "ranks": self.world})
+                            extra={"local_episodes": int(local_c), "ranks": self.world})
 
     def comm_stats(self, clear: bool = True) -> Optional[dict]:
         """The gradient all-reduces timed since comm_events was set to a list (HIP events around the
