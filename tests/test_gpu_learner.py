@@ -344,6 +344,36 @@ def test_epoch_stats_fallback_is_bit_identical(monkeypatch):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("normalize", [True, False])
+def test_graph_replayed_update_is_bit_identical(normalize):
+    """PPOConfig.graph_update (one GPU, minibatches tiling the buffer): each epoch's launches --
+    advantage statistics + per minibatch quad_ppo_grad + quad_clip_adam -- captured once as a
+    hipGraph and replayed per epoch on the epoch's permutation. The same kernels on the same data in
+    the same order as the eager loop: the parameters, Adam moments and loss statistics after two
+    updates (the second all replays) are the same bits. train.py's scale: 8 envs, minibatches of 128."""
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
+    outs = []
+    for graph in (True, False):
+        env = QuadVecEnv(8, env="hover", wrapper="RateControlWrapper", device="cuda:0", seed=3)
+        cfg = PPOConfig(n_steps=256, batch_size=128, n_epochs=3, graph_update=graph, normalize_advantage=normalize)
+        algo = PPO(env, cfg, seed=11)
+        torch.manual_seed(5)
+        sts = []
+        for _ in range(2):
+            algo.collect_rollouts()
+            sts.append(algo.train())
+        assert (algo._epoch_graph is not None) == graph
+        st = algo.opt.state
+        outs.append(([p.detach().clone() for p in algo.policy.parameters()],
+                     [st[p]["exp_avg_sq"].clone() for p in algo.policy.parameters()], sts))
+        env.close()
+    (pa, va, sa), (pb, vb, sb) = outs
+    for a, b in zip(pa + va, pb + vb):
+        assert torch.equal(a, b)
+    assert sa == sb and sa[0]["n"] == 3 * 16
+
+
 @pytest.mark.parametrize("max_norm", [0.5, 1e9, 0.0])
 def test_fused_clip_adam_matches_torch(max_norm):
     """quad_clip_adam (clip_grad_norm_ + Adam.step) vs torch's on identical gradients, 4 steps, on

@@ -3,7 +3,6 @@ import os, sys
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tests"))
-os.environ["QUADENV_LANES"] = sys.argv[1] if len(sys.argv) > 1 else "0"
 import test_gpu_parity as T
 from oracle import oracle as O
 n = 3000; kind = wrap = 0

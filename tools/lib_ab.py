@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Profiling tool (not product): A/B whole-library builds on the step kernel -- `k_step` (QUADENV_LANES=0)
+"""Profiling tool (not product): A/B whole-library builds on the step kernel -- `k_step_h`
 graph-replayed at N envs with each .so given on the command line (one process per library, the
 in-tree library as "base"). Usage: lib_ab.py N lib1.so [lib2.so ...]"""
 import os
@@ -15,8 +15,8 @@ def main():
         from uav_reinforcement_learning_control_amd import _native as N
         if sys.argv[3] != "base":
             N.LIB_PATH = sys.argv[3]
-        from lanes_sweep import run
-        print(f"{os.path.basename(sys.argv[3]):16s} n={sys.argv[2]}: {run(0, int(sys.argv[2]), steps=1000):.2f} us", flush=True)
+        from step_time import run
+        print(f"{os.path.basename(sys.argv[3]):16s} n={sys.argv[2]}: {run(int(sys.argv[2]), steps=1000):.2f} us", flush=True)
         return
     n = sys.argv[1]
     for lib in ["base"] + sys.argv[2:] + ["base"]:

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Profiling tool (not product): A/B of whole-library builds on the one-thread step form (k_step_h
 below 262,144 envs) -- per library (QUADENV_LIB, one process each, interleaved twice) the
-graph-replayed step time at 4,096 and 65,536 envs (tools/lanes_sweep.run) and a digest of every
+graph-replayed step time at 4,096 and 65,536 envs (tools/step_time.run) and a digest of every
 output of 300 stepped steps (obs, reward, flags, terminal obs, state) for each env kind, so that
 a faster variant is also shown to give the same bits. Usage: lib_digest_ab.py lib1.so [lib2.so ...]
 ("base" = the in-tree library)."""
@@ -35,9 +35,8 @@ def digest(env_name, wrapper, info, n=65536, steps=300):
 
 def child():
     sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tools"))
-    os.environ["QUADENV_LANES"] = "0"
-    from lanes_sweep import run
-    t = [min(run(0, n, steps=1000) for _ in range(3)) for n in (4096, 65536)]
+    from step_time import run
+    t = [min(run(n, steps=1000) for _ in range(3)) for n in (4096, 65536)]
     d = [digest("hover", None, "basic"), digest("hover", "RateControlWrapper", "full"),
          digest("trajectory", None, "full"), digest("trajectory", "RateControlWrapper", "basic")]
     import torch

@@ -13,7 +13,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 def child(n, lib, lanes):
     sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tools"))
-    os.environ["QUADENV_LANES"] = lanes
     import torch
     from uav_reinforcement_learning_control_amd import _native as N
     if lib != "base":
@@ -33,8 +32,8 @@ def child(n, lib, lanes):
     g = e.get_state()
     for k in sorted(g):
         h.update(g[k].tobytes())
-    from lanes_sweep import run
-    us = sorted(run(int(lanes), n, steps=1000) for _ in range(3))
+    from step_time import run
+    us = sorted(run(n, steps=1000) for _ in range(3))
     print(f"{os.path.basename(lib):14s} n={n} lanes={lanes}: {us[0]:.2f} us/step (runs "
           f"{', '.join(f'{u:.2f}' for u in us)}) digest {h.hexdigest()[:16]}", flush=True)
 

@@ -19,7 +19,6 @@ sys.path.insert(0, ROOT)
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    os.environ["QUADENV_LANES"] = "0"
     import ctypes as C
     import torch
     from uav_reinforcement_learning_control_amd import _native as N

@@ -6,10 +6,10 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-from lanes_sweep import run  # noqa: E402
+from step_time import run  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 lanes = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-r = sorted(run(lanes, n, steps=1000) for _ in range(3))[0]
-h = sorted(run(lanes, n, steps=1000, hover_actions=True) for _ in range(3))[0]
+r = sorted(run(n, steps=1000) for _ in range(3))[0]
+h = sorted(run(n, steps=1000, hover_actions=True) for _ in range(3))[0]
 print(f"n={n} lanes={lanes}: random actions {r:.2f} us/step, near-hover actions (no resets) {h:.2f} us/step")

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Profiling tool (not product): the step kernel at N envs under several library / form settings,
 one process each (env overrides as KEY=VAL, a library path as LIB=path). Graph-replayed launches,
-HIP events (tools/lanes_sweep.run), best of 3. Usage: sizes_ab.py N "KEY=VAL ..." ["..."]"""
+HIP events (tools/step_time.run), best of 3. Usage: sizes_ab.py N "KEY=VAL ..." ["..."]"""
 import os
 import subprocess
 import sys
@@ -15,10 +15,10 @@ def main():
         from uav_reinforcement_learning_control_amd import _native as N
         if os.environ.get("LIB"):
             N.LIB_PATH = os.environ["LIB"]
-        from lanes_sweep import run
-        lanes = int(os.environ.get("QUADENV_LANES", "1"))
+        from step_time import run
+
         n = int(sys.argv[2])
-        t = min(run(lanes, n, steps=400) for _ in range(3))
+        t = min(run(n, steps=400) for _ in range(3))
         dg = ""
         if os.environ.get("DIGEST"):  # every output of 40 stepped steps: forms must agree bit for bit
             import hashlib

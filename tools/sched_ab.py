@@ -8,9 +8,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if len(sys.argv) > 1 and sys.argv[1] == "child":
     sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from lanes_sweep import run
-    print(f"{os.path.basename(os.environ['QUADENV_LIB']):18s} 65536: {run(0, 65536, steps=1000):.3f} us   "
-          f"1M: {run(1, 1048576, steps=200):.2f} us   4M: {run(1, 4194304, steps=100):.1f} us", flush=True)
+    from step_time import run
+    print(f"{os.path.basename(os.environ['QUADENV_LIB']):18s} 65536: {run(65536, steps=1000):.3f} us   "
+          f"1M: {run(1048576, steps=200):.2f} us   4M: {run(4194304, steps=100):.1f} us", flush=True)
     sys.exit(0)
 libs = sys.argv[1:]
 for rep in range(2):

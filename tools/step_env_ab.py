@@ -19,7 +19,6 @@ def child(n, spec):
     for kv in filter(None, envs.split(",")):
         k, v = kv.split("=")
         os.environ[k] = v
-    os.environ.setdefault("QUADENV_LANES", "0")
     sys.path.insert(0, ROOT)
     import torch
     from uav_reinforcement_learning_control_amd import _native as N

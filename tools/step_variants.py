@@ -24,12 +24,11 @@ def main():
 
 
 def child(n, lanes, v):
-    os.environ["QUADENV_LANES"] = lanes
     from uav_reinforcement_learning_control_amd import _native as N
     if v != "base":
         N.LIB_PATH = os.path.join(ROOT, "tools", "_build", f"abl_{v}.so")
-    from tools.lanes_sweep import run
-    us = [run(int(lanes), n, steps=400) for _ in range(3)]
+    from tools.step_time import run
+    us = [run(n, steps=400) for _ in range(3)]
     print(f"{v:8s} n={n} lanes={lanes}: {min(us):.2f} us/step (runs {', '.join(f'{u:.2f}' for u in us)})")
 
 

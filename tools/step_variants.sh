@@ -1,7 +1,7 @@
 #!/bin/bash
 # Profiling tool (not product): build cost-ablation variants of libquadenv.so for
 # tools/step_variants.py -- the physics run twice / skipped, the observation (scipy Euler) skipped,
-# the auto-reset branch compiled out (k_step, QUADENV_LANES=0), the SLP vectorizer on. Output: tools/_build/abl_*.so
+# the auto-reset branch compiled out (k_step_h), the SLP vectorizer on. Output: tools/_build/abl_*.so
 # (the rollout / learner objects are the product's, from csrc/Makefile's _lib/obj)
 set -e
 cd "$(dirname "$0")/../uav_reinforcement_learning_control_amd/csrc"

@@ -1353,9 +1353,11 @@ int quad_step_random(QuadHandle* h, uint32_t step0, int32_t steps, const QuadSte
     hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, true, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);  \
   else                                                                                                   \
     hipLaunchKernelGGL((k_step_random_h<QUAD_ENV_HOVER, false, SP, RB>), grid, blk2, 0, s, h->kdev, h->kp, *out, ao, step0, steps);
-  // the block size of k_step_h's policy (h_wide: 64-env blocks up to H_SMALL and from 2M envs);
-  // the K-step form reads and writes its state once per launch, so the nt policy does not apply
-  const bool wide = h_wide(h, h->n);
+  // 64-env blocks up to H_SMALL envs, 256 above at every size: the K-step form reads and writes its
+  // state once per launch, so k_step_h's reason for 64-env blocks from 2M envs (nt state streams)
+  // does not apply -- 2M envs 93.6 vs 97.4 us per step, 4M 182.9 vs 195.7 with 64-env blocks
+  // (profiles/r06/kstep_random_block_ab.txt). QUADENV_HBLOCK pins it.
+  const bool wide = h->hblock ? h->hblock == 256 : h->n > H_SMALL;
   if (!wide) {
     const dim3 grid(unsigned((int64_t(h->n) + 63) / 64)), blk2(128);
     if (h->spec) { QD_LAUNCH_RH(true, 64) } else { QD_LAUNCH_RH(false, 64) }

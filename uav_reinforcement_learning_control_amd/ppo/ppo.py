@@ -55,6 +55,7 @@ class PPOConfig:
     fused_rollout: bool = True            # whole rollout as quad_rollout launches (needs fused_policy)
     rollout_chunk: int = 1024             # steps per quad_rollout launch
     fused_update: bool = True             # minibatch gradient on MFMA (ppo/learner.py, quad_ppo_grad)
+    graph_update: bool = True             # single GPU: replay each epoch's optimizer steps as one hipGraph
 
 
 # quad_ppo_adv_stats_epoch's grid y limit is 65,535; its [n, 512] float64 output is 4 KB per
@@ -69,14 +70,15 @@ def n_minibatches(total: int, batch: int) -> int:
     return max(1, -(-int(total) // int(batch)))
 
 
-def epoch_permutation(total: int, device: torch.device) -> torch.Tensor:
+def epoch_permutation(total: int, device: torch.device, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The epoch's minibatch order (SB3 PPO.train: np.random.permutation(buffer_size)). On a ROCm
     GPU it is quad_permutation -- a keyed Feistel bijection of [0, total) computed one index per
     thread (torch.randperm sorts `total` random keys: 5.3 ms per epoch at config 3). The key is drawn
     from torch's default CPU generator, so torch.manual_seed fixes it and no device sync happens."""
     if device.type != "cuda":
         return torch.randperm(total, device=device)
-    out = torch.empty(total, dtype=torch.int64, device=device)
+    if out is None:
+        out = torch.empty(total, dtype=torch.int64, device=device)
     seed = int(torch.randint(0, 2**62, (1,), dtype=torch.int64))
     N.check(N.lib().quad_permutation(total, seed, out.data_ptr(), torch.cuda.current_stream(device).cuda_stream),
             "quad_permutation")
@@ -246,6 +248,7 @@ class PPO:
                                       self.cfg.normalize_advantage)
                          if self.cfg.fused_update and fusable and self.device.type == "cuda" else None)
         self._adam = FusedAdam(self.opt, self.cfg.max_grad_norm) if self._learner is not None else None
+        self._epoch_graph = None  # (key, graph, perm, sums, mstats) of _train_fused's captured epoch
         self._t_host = 0  # running step counter of the one-launch path (keys the action noise)
         self._cursor_resume = None  # the two-launch path's noise counter after load_state_dict
         self._noise_seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x5851F42D4C957F2D) & (2**64 - 1)
@@ -456,6 +459,9 @@ class PPO:
         minibatch copies), the flat-bucket all-reduce, then clip_grad_norm_ + Adam as quad_clip_adam."""
         cfg = self.cfg
         total = obs.shape[0]
+        if (cfg.graph_update and self.world == 1 and max_minibatches is None and total % B == 0
+                and 1 <= nmb <= EPOCH_STATS_MAX_MINIBATCHES and epochs >= 1):
+            return self._train_graphed(obs, act, logp_old, adv, ret, B, nmb, epochs, stats)
         steps = epochs * nmb if max_minibatches is None else min(epochs * nmb, max_minibatches)
         mstats = torch.zeros(max(steps, 1), 4, dtype=torch.float32, device=self.device)
         perms, sums = {}, {}
@@ -488,6 +494,53 @@ class PPO:
             done += 1
         a = mstats[:done].double().mean(0).tolist() if done else [0.0] * 4
         stats.update(pg_loss=a[0], vf_loss=a[1], entropy=a[2], clip_fraction=a[3], n=done)
+        return stats
+
+    def _epoch_steps(self, obs, act, logp_old, adv, ret, B, nmb, perm, sums, mstats) -> None:
+        """One epoch of the fused update on fixed buffers: the epoch's advantage statistics (one
+        launch), then per minibatch quad_ppo_grad + quad_clip_adam -- the launch sequence
+        _train_fused issues, on the permutation in `perm`."""
+        if self._learner.normalize_advantage:
+            self._learner.adv_stats_epoch(adv, perm, B, nmb, out=sums)
+        for m in range(nmb):
+            self._learner.grads(obs, act, logp_old, adv, ret, perm[m * B:(m + 1) * B], mstats[m],
+                                adv_sums=sums[m] if self._learner.normalize_advantage else None)
+            self._adam.step()
+
+    def _train_graphed(self, obs, act, logp_old, adv, ret, B, nmb, epochs, stats) -> dict:
+        """_train_fused for one GPU when the minibatches tile the buffer: every epoch's launches
+        (advantage statistics + nmb x (quad_ppo_grad + quad_clip_adam)) captured once as a hipGraph
+        on persistent permutation / statistics buffers and replayed per epoch after the epoch's
+        permutation is drawn into its buffer -- the same kernels on the same data in the same
+        order as the eager loop (the same bits), without its per-launch host work (at train.py's
+        scale, 8 envs x 1,024 steps in minibatches of 128, that host work was most of the update).
+        The first epoch after a (re)capture runs eagerly; its launches warm the workspaces."""
+        total, dev = obs.shape[0], self.device
+        key = (B, nmb, obs.data_ptr(), adv.data_ptr(), self._learner.normalize_advantage)
+        mstats = torch.zeros(epochs * nmb, 4, dtype=torch.float32, device=dev)
+        e0 = 0
+        if self._epoch_graph is None or self._epoch_graph[0] != key:
+            perm = torch.empty(total, dtype=torch.int64, device=dev)
+            sums = torch.empty(nmb, N.ADV_SUM_DOUBLES, dtype=torch.float64, device=dev)
+            mst = torch.zeros(nmb, 4, dtype=torch.float32, device=dev)
+            epoch_permutation(total, dev, out=perm)
+            self._epoch_steps(obs, act, logp_old, adv, ret, B, nmb, perm, sums, mstats[:nmb])
+            e0 = 1
+            g = torch.cuda.CUDAGraph()
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    self._epoch_steps(obs, act, logp_old, adv, ret, B, nmb, perm, sums, mst)
+            torch.cuda.current_stream(dev).wait_stream(s)
+            self._epoch_graph = (key, g, perm, sums, mst)
+        _, g, perm, sums, mst = self._epoch_graph
+        for e in range(e0, epochs):
+            epoch_permutation(total, dev, out=perm)
+            g.replay()
+            mstats[e * nmb:(e + 1) * nmb].copy_(mst)
+        a = mstats.double().mean(0).tolist()
+        stats.update(pg_loss=a[0], vf_loss=a[1], entropy=a[2], clip_fraction=a[3], n=epochs * nmb)
         return stats
 
     def learn(self, total_timesteps: int, callback: Optional[Callable] = None) -> "PPO":
