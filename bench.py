@@ -210,7 +210,8 @@ def _run_rank(args, rank, world, local_rank):
             "config2_hover_4096_one_launch": _kstep_rate(4096, 1000, dev, args.seed),
             "hover_65536_one_launch_random": _kstep_rate(65536, 200, dev, args.seed),
             "config5_traj_ctbr_65536": _kernel_rate(65536, "trajectory", "RateControlWrapper", dev, args.seed),
-            "hover_ctbr_65536": _kernel_rate(65536, "hover", "RateControlWrapper", dev, args.seed)}
+            "hover_ctbr_65536": _kernel_rate(65536, "hover", "RateControlWrapper", dev, args.seed),
+            "config1_train_py_on_gpu": _train_py_scale(dev, args.seed)}
     del actions, g
     env.close()
     if rank == 0:
@@ -302,6 +303,38 @@ def _kernel_rate(n, kind, wrapper, dev, seed) -> dict:
     bpe = BYTES_PER_ENV_STEP + (24 if wrapper else 0)
     return {"envs": n, "env": kind, "wrapper": wrapper, "kernel_us": us,
             "env_steps_per_s": n / (us * 1e-6), "achieved_GBs": bpe * n / (us * 1e-6) / 1e9}
+
+
+def _train_py_scale(dev, seed, iters: int = 2) -> dict:
+    """SURVEY config 1's workload -- train.py's PPO iteration (16 HoverEnv + RateControlWrapper envs x
+    1,024 steps, then 20 epochs x 128 minibatches of 128 rows = 2,560 Adam steps) -- on the GPU path
+    (quad_rollout, quad_ppo_grad, quad_clip_adam; each epoch's optimizer steps one hipGraph replay),
+    beside cpu_baseline_ppo's CPU timing of the same iteration. One untimed iteration first."""
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    from uav_reinforcement_learning_control_amd.ppo import PPO, PPOConfig
+    env = QuadVecEnv(16, env="hover", wrapper="RateControlWrapper", device=dev, seed=seed)
+    m = PPO(env, PPOConfig(batch_size=128), seed=0)
+    m.collect_rollouts()
+    m.train()
+    torch.cuda.synchronize()
+    t_roll = t_train = 0.0
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        rs = m.collect_rollouts()
+        t1 = time.perf_counter()
+        m.train()
+        torch.cuda.synchronize()
+        t_roll += t1 - t0
+        t_train += time.perf_counter() - t1
+    steps = rs.env_steps
+    opt_steps = m.cfg.n_epochs * m.n_minibatches_per_epoch()
+    out = {"envs": 16, "n_steps": m.cfg.n_steps, "batch_size": m.batch, "optimizer_steps": opt_steps,
+           "rollout_s": t_roll / iters, "train_s": t_train / iters,
+           "us_per_optimizer_step": 1e6 * t_train / iters / opt_steps,
+           "env_steps_per_s": steps * iters / (t_roll + t_train), "graph_update": m._epoch_graph is not None}
+    del m
+    env.close()
+    return out
 
 
 def _kstep_rate(n, steps, dev, seed) -> dict:
@@ -924,7 +957,43 @@ def main():
         line["cpu_baseline_all_cores"] = _cpu_baseline(args.cpu_seconds, cores)
         line["cpu_baseline_ppo"] = _cpu_baseline_ppo(args.cpu_seconds, 1)
         line["cpu_baseline_ppo_all_cores"] = _cpu_baseline_ppo(args.cpu_seconds, cores)
+    line["summary"] = _summary(line)  # last: the driver keeps the tail of stdout
     print(json.dumps(line), flush=True)
+
+
+def _summary(line: dict) -> dict:
+    """The line's key figures in a few hundred bytes, printed as its last key (the driver records
+    only the last 2,000 characters of stdout; the full objects above precede it)."""
+    def g(*path):
+        x = line
+        for k in path:
+            if not isinstance(x, dict) or k not in x:
+                return None
+            x = x[k]
+        return round(x, 4) if isinstance(x, float) else x
+    return {
+        "step_value": g("value"), "step_kernel_us": g("roofline", "kernel_us"), "step_frac": g("roofline", "frac"),
+        "step_frac_beyond_launch_floor": g("roofline", "frac_beyond_launch_floor"),
+        "launch_floor_us": g("roofline", "launch_floor_us"),
+        "rollout_env_steps_per_s": g("rollout_phase", "env_steps_per_s"),
+        "rollout_kernel_us_per_step": g("rollout_phase", "rollout_kernel", "us_per_step"),
+        "rollout_matrix_pipe_frac": g("rollout_phase", "rollout_kernel", "matrix_pipe_frac"),
+        "e2e_env_steps_per_s": g("end_to_end", "env_steps_per_s"), "e2e_train_s": g("end_to_end", "train_s"),
+        "e2e_rollout_s": g("end_to_end", "rollout_s"),
+        "learner_us_per_minibatch": g("end_to_end", "learner_kernel", "us_per_minibatch"),
+        "learner_matrix_pipe_frac": g("end_to_end", "learner_kernel", "matrix_pipe_frac"),
+        "large_1M_kernel_us": g("large_batch", "kernel_us"), "large_1M_frac": g("large_batch", "frac"),
+        "dram_4M_kernel_us": g("large_batch_dram", "kernel_us"), "dram_4M_frac": g("large_batch_dram", "frac"),
+        "dram_4M_copy_floor_us": g("large_batch_dram", "copy_floor_us"),
+        "dram_4M_frac_of_copy_floor": g("large_batch_dram", "frac_of_copy_floor"),
+        "config2_4096_one_launch_us_per_step": g("configs", "config2_hover_4096_one_launch", "us_per_step"),
+        "config5_traj_ctbr_us": g("configs", "config5_traj_ctbr_65536", "kernel_us"),
+        "config1_on_gpu_env_steps_per_s": g("configs", "config1_train_py_on_gpu", "env_steps_per_s"),
+        "cpu_baseline": g("cpu_baseline", "value"), "cpu_baseline_ppo": g("cpu_baseline_ppo", "value"),
+        "per_rank_elapsed_max_over_min": g("per_rank", "elapsed_s", "max_over_min"),
+        "per_rank_slowest": g("per_rank", "elapsed_s", "argmax_rank"),
+        "allreduce_median_us": g("end_to_end", "allreduce", "median_us"),
+    }
 
 
 if __name__ == "__main__":

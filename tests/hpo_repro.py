@@ -286,6 +286,8 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawTextHelpFormatter)
     ap.add_argument("--path", choices=["gpu", "cpu"])
     ap.add_argument("--seeds", type=int, nargs="+", default=[0])
+    ap.add_argument("--n-envs", type=int, default=8,
+                    help="training envs (optimize.py's --n-envs: default 8; optimize.sh passes 16, train.py uses 16)")
     ap.add_argument("--permutation", choices=["feistel", "randperm"], default="feistel",
                     help="GPU path's epoch permutation: quad_permutation (the product) or torch.randperm")
     ap.add_argument("--wrapper", choices=sorted(WRAPPERS), default="RateControlWrapper",
@@ -301,6 +303,8 @@ def main(argv=None) -> int:
             key = d["path"] if d.get("wrapper", "RateControlWrapper") == "RateControlWrapper" else f'{d["path"]}_{d["wrapper"]}'
             if d.get("permutation", "feistel") != "feistel":
                 key += "_" + d["permutation"]
+            if d.get("n_envs", 8) != 8:
+                key += f'_{d["n_envs"]}envs'
             runs.setdefault(key, []).extend(d["runs"])
         for rs in runs.values():
             rs.sort(key=lambda r: r["seed"])
@@ -313,11 +317,11 @@ def main(argv=None) -> int:
                 torch.randperm(total, device=device) if out is None else out.copy_(torch.randperm(total, device=device)))
         rs = []
         for s in a.seeds:
-            r = fn(s, wrapper=a.wrapper)
+            r = fn(s, n_envs=a.n_envs, wrapper=a.wrapper)
             print(f"[{a.path} {a.wrapper} seed {s}] {r['seconds']:.1f} s  curve "
                   + " ".join(f"{v:.1f}" for v in r["curve"]), flush=True)
             rs.append(r)
-        res = {"path": a.path, "wrapper": a.wrapper, "permutation": a.permutation, "runs": rs}
+        res = {"path": a.path, "wrapper": a.wrapper, "permutation": a.permutation, "n_envs": a.n_envs, "runs": rs}
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """A/B tool (not product): SHA-256 digests of every output of the env kernels under each given
 library build -- so a refactor or a schedule change can be shown to give identical bits. One
-process per library: 40 quad_step launches (each step form: k_step_h 64/256-env blocks, k_step,
-k_step_g<1>/<2>; hover, hover + CTBR, trajectory + CTBR) with random actions and auto-resets, every
+process per library: 40 quad_step launches (each step form, pinned: k_step_h in 64/256-env blocks,
+the 64-env nt form, k_step_hd; hover, hover + CTBR, trajectory + CTBR) with random actions and auto-resets, every
 obs / reward / flag / terminal obs and the final state; and a 32-step quad_rollout (one launch).
 Usage: env_digest.py lib1.so [lib2.so ...]"""
 import hashlib

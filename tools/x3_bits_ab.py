@@ -2,7 +2,8 @@
 """A/B tool (not product): the bits of quad_ppo_grad's gradients under each given library build --
 one process per library computes every parameter's .grad on the same seeded 524,288-row minibatch
 (config 3's shape, three minibatches of one permutation) and prints a SHA-256 of the gradient bytes
-and the stats, so a rebuilt learner can be shown to give identical results. Usage:
+and the stats, so a rebuilt learner can be shown to give identical results; X3_BITS_B=128 (say)
+takes minibatches of that many rows instead (the small-batch launch form). Usage:
 x3_bits_ab.py lib1.so [lib2.so ...]"""
 import hashlib
 import os
@@ -22,7 +23,8 @@ def child(lib):
     from uav_reinforcement_learning_control_amd.ppo.ppo import PPOConfig
     torch.manual_seed(0)
     cfg = PPOConfig()
-    B, M = 524288, 65536 * 32
+    B = int(os.environ.get("X3_BITS_B", 524288))
+    M = max(65536 * 32 if B == 524288 else 8 * B, 3 * B)
     pol = ActorCritic().cuda()
     g = torch.Generator(device="cuda").manual_seed(1)
     obs = torch.rand(M, 12, device="cuda", generator=g) * 2 - 1
@@ -40,7 +42,7 @@ def child(lib):
         for p in pol.parameters():
             h.update(p.grad.detach().cpu().numpy().tobytes())
         h.update(stats.cpu().numpy().tobytes())
-    print(f"{os.path.basename(lib)}: {h.hexdigest()[:32]}", flush=True)
+    print(f"{os.path.basename(lib)} (B = {B}): {h.hexdigest()[:32]}", flush=True)
 
 
 def main():

@@ -159,7 +159,8 @@ def _declare(L):
     L.quad_observe.argtypes = [vp, vp, vp, vp]
     L.quad_terminated.argtypes = [vp, vp, i32, vp, vp]
     L.quad_step_random.argtypes = [vp, u32, i32, C.POINTER(QuadStepOut), vp, vp]
-    L.quad_mem_floor.argtypes = [vp, vp, C.POINTER(QuadStepOut), vp]
+    if hasattr(L, "quad_mem_floor"):  # (added in round 6 as a backward-compatible entry; A/B tools load older builds)
+        L.quad_mem_floor.argtypes = [vp, vp, C.POINTER(QuadStepOut), vp]
     L.quad_kernel_form.argtypes = [vp]
     L.quad_kernel_form.restype = i32
     L.quad_random_actions.argtypes = [vp, u32, vp, vp]
@@ -190,7 +191,6 @@ def _declare(L):
     L.quad_adam_workspace_bytes.restype = C.c_int64
     L.quad_clip_adam.argtypes = [C.POINTER(QuadAdam), vp, C.c_int64, vp]
     for n in ("quad_clip_adam", "quad_ppo_grad", "quad_ppo_hidden", "quad_ppo_adv_stats", "quad_ppo_adv_stats_epoch", "quad_default_cfg", "quad_create", "quad_seed", "quad_reset", "quad_step", "quad_step_range", "quad_observe", "quad_terminated", "quad_step_random",
-           "quad_mem_floor",
               "quad_random_actions", "quad_get_state", "quad_set_state", "quad_gae",
               "quad_policy_pack", "quad_policy_act", "quad_rollout_post", "quad_rollout",
               "quad_waypoints_begin", "quad_waypoints_update"):

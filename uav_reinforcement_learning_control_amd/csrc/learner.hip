@@ -49,10 +49,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int SH = 130;       // row stride (floats) of the [row][neuron] images
 constexpr int SO = 13;        // row stride of the observation image (odd: conflict-free columns)
-#ifndef QD_LRN_ACTOR_SHARE
-#define QD_LRN_ACTOR_SHARE 540  // measured: 500 -> 1.30 ms, 525 -> 1.26, 540 -> 1.22-1.25, 550 -> 1.23, 580 -> 1.32
-#endif
-constexpr int ACTOR_SHARE = QD_LRN_ACTOR_SHARE;  // per mille of the block slots that run the actor
+// measured: 500 -> 1.30 ms, 525 -> 1.26, 540 -> 1.22-1.25, 550 -> 1.23, 580 -> 1.32
+constexpr int ACTOR_SHARE = 540;  // per mille of the block slots that run the actor
 
 // LDS image (floats)
 constexpr int L_H1 = 0, L_DH2 = L_H1 + RND * SH, L_H2 = L_DH2 + RND * SH;

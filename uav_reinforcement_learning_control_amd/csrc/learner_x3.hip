@@ -106,10 +106,7 @@ __global__ __launch_bounds__(256) void k_x3_prep(const float* __restrict__ wa, c
 
 // how many k-steps ahead L2 / dh1 load their pre-split W2 pieces (global loads, L2-resident); round 5
 // A/B (profiles/r05/learner_wpf_ab.txt): 3 is 5 % slower (register pressure), 1 the same as 2
-#ifndef QD_X3_WPF
-#define QD_X3_WPF 2
-#endif
-constexpr int WPF = QD_X3_WPF, WRING = WPF + 1;
+constexpr int WPF = 2, WRING = WPF + 1;
 static_assert(WPF >= 1 && WPF <= 3, "prefetch distance");
 
 // QD_LPROBE (tools/probe/probe_learner.py builds only, never the product): the dump build records
@@ -573,11 +570,7 @@ __device__ __forceinline__ void body(const GArgs& g, char* __restrict__ L, int b
         }
 #pragma unroll
         for (int t = 0; t < 2; t++) {
-#if defined(QD_X3_DH1ONE)
-          dh1[t] = mma3(a[t], wr1[s % WRING], dh1[t]);
-#else
           mma3s(a[t], wr1[s % WRING], dh1[t], dh1s[t]);
-#endif
         }
         if (s + WPF < 8) X3_PIPE_V(3, 6, 12);
         else if (s < 7) X3_PIPE(6, 12);
@@ -706,6 +699,19 @@ __global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3(GArgs g) {
   body<1>(g, lds_x3, blockIdx.x);
 }
 
+// small minibatches (2 nb <= X3_BLOCKS: at most 128 rounds, 8,192 rows): the actor's and the critic's
+// rounds of the same rows in separate blocks of one launch (blocks [0, nb) actor, [nb, 2 nb) critic),
+// so a block runs one net and the launch lasts half as long -- the same rows per block and net as
+// k_ppo_grad_x3, the same partial slots, so the same bits. train.py's minibatches of 128 rows are two
+// rounds: two blocks each running both nets left 254 of the 256 CUs idle for both nets' latency.
+__global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3_sep(GArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds_x3s[];
+  if (int(blockIdx.x) < g.nb)
+    body<ACT>(g, lds_x3s, blockIdx.x);
+  else
+    body<1>(g, lds_x3s, blockIdx.x - g.nb);
+}
+
 // diagnostics: the same body with the hidden pre-activations recorded (quad_ppo_hidden)
 __global__ __launch_bounds__(LB, 1) void k_ppo_grad_x3_dump(GArgs g) {
   extern __shared__ __attribute__((aligned(16))) char lds_x3d[];
@@ -738,7 +744,9 @@ int launch_ppo_grad_x3(const GArgs& g, hipStream_t s, double* adv_stats, const f
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return set_error(QUAD_EHIP, "hipGetDevice failed");
   if (!opted[dev]) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_x3), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            B_TOTAL) != hipSuccess)
+                            B_TOTAL) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ppo_grad_x3_sep),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, B_TOTAL) != hipSuccess)
       return set_error(QUAD_EHIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     opted[dev] = true;
   }
@@ -771,7 +779,10 @@ int launch_ppo_grad_x3(const GArgs& g, hipStream_t s, double* adv_stats, const f
       return set_error(QUAD_EHIP, "learner split: join failed");
     return QUAD_OK;
   }
-  hipLaunchKernelGGL(k_ppo_grad_x3, dim3(g.nb), dim3(LB), B_TOTAL, s, g);
+  if (2 * g.nb <= X3_BLOCKS && g.nbc == g.nb)
+    hipLaunchKernelGGL(k_ppo_grad_x3_sep, dim3(2 * g.nb), dim3(LB), B_TOTAL, s, g);
+  else
+    hipLaunchKernelGGL(k_ppo_grad_x3, dim3(g.nb), dim3(LB), B_TOTAL, s, g);
   if (hipGetLastError() != hipSuccess) return set_error(QUAD_EHIP, "k_ppo_grad_x3 launch failed");
   return QUAD_OK;
 }

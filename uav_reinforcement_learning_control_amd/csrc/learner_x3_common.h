@@ -149,10 +149,6 @@ static_assert(int64_t(2 * 4 * 2 * 8 * 3 * 64) * 16 == WIMG_BYTES, "pre-split ima
 // sum gave the forward outputs a systematic bias of up to ~48 ulp over a 128-deep product, which
 // the minibatch sums of the bias / head gradients accumulate linearly. The caller adds sm once.
 __device__ __forceinline__ void mma3s(const X3& a, const X3& b, f32x16& big, f32x16& sm) {
-#if defined(QD_X3_ONEACC)  // A/B builds only: the single-accumulator order
-  big = mma3(a, b, big);
-  return;
-#endif
   sm = mfma16(a.p[2], b.p[0], sm);
   sm = mfma16(a.p[1], b.p[1], sm);
   sm = mfma16(a.p[0], b.p[2], sm);

@@ -131,9 +131,7 @@ __device__ __forceinline__ void store_target_info(float* __restrict__ out, int i
 // measured equal (5.84-5.87 vs 5.83-5.87 us) and 128 slower (6.10), so batches above H_SMALL keep
 // 256 (profiles/r02/ab_step_h_block.txt).
 constexpr int H_SMALL = 32768;
-#ifndef QD_H_PRE
-#define QD_H_PRE 1  // Philox blocks of the helper's reset draw issued before barrier (C): 1 measured best (below)
-#endif
+constexpr int H_PRE = 1;  // Philox blocks of the helper's reset draw issued before barrier (C): 1 measured best (below)
 // Small batches (64-env blocks, default cache policy: up to H_SMALL envs): each step lane stores its
 // own obs row (three 16-byte stores; the non-resetting lanes before barrier 1, under the helper's
 // reset draw) instead of the block's LDS transpose + barrier 2 + the shared copy -- 3.38 vs 3.45-3.46
@@ -145,15 +143,11 @@ constexpr bool obs_direct() { return HB == 64 && !NT; }
 // writes an env's 28 image words as seven 16-byte stores (and its control words as two) and a
 // resetting step lane reads its row back the same way, instead of one word per field; same bits,
 // 4,096 envs 3.32 vs 3.36 us, 4M 249.8-250.6 vs 253.8-254.6, 65,536 and 1M unchanged
-// (profiles/r05/step_rowmajor_image_ab.txt). QD_H_ROWMAJOR=0: the field-major layout (A/B builds)
-#ifndef QD_H_ROWMAJOR
-#define QD_H_ROWMAJOR 1
-#endif
-// H / CT layout: field-major [f][HB], or (QD_H_ROWMAJOR, no CTBR) 16-byte env rows (H: 28 words, CT:
-// CT_STRIDE); the CTBR kinds keep the field-major forms (config 5 at 65,536 envs measured 5.92 vs
-// 5.78 us with row-major H)
+// (profiles/r05/step_rowmajor_image_ab.txt).
+// H / CT layout: 16-byte env rows (H: 28 words, CT: CT_STRIDE) without CTBR; the CTBR kinds keep the
+// field-major [f][HB] forms (config 5 at 65,536 envs measured 5.92 vs 5.78 us with row-major H)
 template <bool CTBR>
-constexpr bool ct_rows() { return QD_H_ROWMAJOR && !CTBR; }
+constexpr bool ct_rows() { return !CTBR; }
 constexpr int CT_STRIDE = 8;  // words per env row of CT (6 used)
 constexpr int HROW = 28;  // floats per env in the helper image: pos 3, quat 4, v 3, w 3, target 3, obs 12
 constexpr int HCTL = 9;   // floats per env from the control helper: Fsum, taum 3, volt, bad ctrl, rint 3
@@ -224,7 +218,7 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     }
     // (R) env i's next reset, into H[f][l]: the first PRE Philox blocks before barrier (C), at
     // normal priority, in the slack the helper has while the step wave accumulates forward_base
-    constexpr int PRE = QD_H_PRE;
+    constexpr int PRE = H_PRE;
     float u16[16];
     if (PRE > 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
@@ -269,15 +263,6 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
   } else {  // ---- step
     float obs[12];
     EnvRegs<float> e;
-#if defined(QD_H_NOCTL)  // A/B builds only: the step wave runs the control path itself (round 2)
-    load_env<AUX>(p, i, e, CTBR);
-    const uint32_t ep = S.ldu(F_EP, vo);
-    const float4 a4 = act[i];
-    const float a[4] = {a4.x, a4.y, a4.z, a4.w};
-    StepRes r;
-    env_step<float, CTBR>(K, e, a, r);
-    __syncthreads();  // (C)
-#else
     load_env_motion<AUX>(p, i, e);
     const uint32_t ep = S.ldu(F_EP, vo);
     if (stamps) { QD_PIN(ep); QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.th, 4); QD_PIN_N(e.v, 3);
@@ -323,7 +308,6 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     QD_STAMP(stamps, 4);
     StepRes r;
     env_post(K, e, r);
-#endif
     if (stamps) { QD_PIN_N(r.obs, 12); QD_PIN(r.reward); QD_PIN(uint32_t(r.term)); }
     QD_STAMP(stamps, 5);
     settle(ep);
