@@ -2,7 +2,7 @@
 # Profiling tool (not product): the step kernel's counted issue roofline. rocprofv3 PMC passes
 # (one counter group per run, SQ <= 8 and GRBM <= 2 per pass) over tools/step_once.py -- eager
 # quad_step launches, random actions -- at the sizes in $SIZES (default 65,536 envs: k_step_h, one
-# step wave per SIMD; 1,048,576 and 4,194,304: k_step_g<1>); then tools/pmc/issue_roofline.py writes
+# step wave per SIMD; 1,048,576: k_step_h, 256-env blocks; 4,194,304: k_step_hd); then tools/pmc/issue_roofline.py writes
 # profiles/<round>/pmc_issue.json and profiles/pmc_issue.json (read by bench.py, keyed by kernel
 # symbol and env count). Every pass runs under its own time limit; a failing pass ends the script.
 set -u

@@ -3,7 +3,7 @@
 # rocprofv3 PMC passes, one counter group per run (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2, so
 # they never share a pass), over tools/step_once.py (eager quad_step launches, random actions,
 # auto-reset on) at 65,536 envs (k_step_h, the bench's N=1 kernel), 1,048,576 and 4,194,304 envs
-# (k_step_g<1>), plus the dword-per-lane calibration copy (tools/pmc/pmc_calib.hip) whose byte count
+# (k_step_h, 256-env blocks; k_step_hd), plus the dword-per-lane calibration copy (tools/pmc/pmc_calib.hip) whose byte count
 # is known. EXTRA="<counter> ..." adds one pass per listed counter (e.g. DRAM-side TCC counters).
 # tools/pmc/traffic_summary.py turns the CSVs into profiles/<round>/pmc_traffic.json.
 # Every pass runs under its own time limit; a failing pass ends the script.
