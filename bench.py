@@ -372,7 +372,9 @@ def _end_to_end(env, args, world: int = 1) -> dict:
     m = PPO(env, cfg, seed=0)
     first = m.collect_rollouts(use_graph=True)  # capture + warm (not timed)
     first_stats = m._done_stats.tolist()  # the whole job's (reduced over ranks), before any update
-    m.train(n_epochs=1, max_minibatches=2)
+    # warm-up (not timed): on one GPU two epochs capture the update's per-epoch hipGraph (PPO.
+    # _train_graphed; setup, like the rollout's graph capture above); otherwise two minibatches
+    m.train(n_epochs=2) if world == 1 and m._learner is not None else m.train(n_epochs=1, max_minibatches=2)
     torch.cuda.synchronize()
     t_roll = t_train = 0.0
     if world > 1:

@@ -193,7 +193,7 @@ QD_HD float div_const(float a, float b, float rb) {
 
 // np.clip semantics: NaN propagates
 // (two flat selects: NaN fails both compares and passes through; lo <= hi. The nested form with an
-// explicit NaN test compiled to divergent branches -- 20 exec-mask regions per k_step.)
+// explicit NaN test compiled to divergent branches -- 20 exec-mask regions per step.)
 template <typename T>
 QD_HD T clipn(T x, T lo, T hi) {
   const T a = x < lo ? lo : x;
@@ -376,7 +376,7 @@ QD_HD void box_drag(const T w[3], const T u[3], const T kqa[3], const T kva, con
 //                   accumulated from zero in that order; the props' spin-axis drag torques Qs
 //   forward_finish: + the motor wrench (total thrust along base z, torque), velocity products,
 //                   3x3 solve -> vdot (world), wdot (body), sdot[4]
-// Every step form (k_step, k_step_h, k_step_random*, k_step_relpos, k_rollout) calls both in
+// Every step form (k_step_h / k_step_hd, k_step_random_h, k_step_relpos, k_rollout) calls both in
 // this order, so they compute the same bits whichever wave runs the control path.
 template <typename T>
 struct ForceAcc {

@@ -9,9 +9,9 @@
 // Why one launch: every piece of that loop is per env -- no env ever reads another env's data --
 // so a 256-env block can run ALL the steps of its envs without a grid-wide barrier. The block
 // stages the packed actor + critic (152 KB) into LDS once, keeps each env's state (one env per
-// thread, k_step's form) and its observation in registers across steps, and per step only
+// thread, as the step kernels) and its observation in registers across steps, and per step only
 // WRITES its buffer rows to HBM (80 B per env-step). The two-launch form (k_policy_act with the
-// fused epilogue + k_step) re-stages the weights, reloads and restores the env state and round-
+// fused epilogue + k_step_h) re-stages the weights, reloads and restores the env state and round-
 // trips the observation and action through HBM on every step, and pays two launches per step.
 //
 // Wave w of a block owns envs 64w .. 64w + 63, which are exactly the two 32-env MFMA tiles the
@@ -61,8 +61,8 @@ __device__ __forceinline__ void fragments(const float ob[12], float (&xb)[NT][8]
   }
 }
 
-// The reset draws of the wave's resetting envs, compacted across the wave as in k_step
-// (quadenv.hip reset_words_wave): one Philox pass of (env, block) items for up to 16 resetting
+// The reset draws of the wave's resetting envs, compacted across the wave (the round-1..5 one-wave
+// step kernel did the same through LDS): one Philox pass of (env, block) items for up to 16 resetting
 // envs. The words travel by lane shuffles instead of LDS (the nets fill it). Identical words.
 // `publish`: this lane lists its env (one lane per env); `apply`: this lane takes the words of the
 // env listed under key `key` (KEY_MASK = 31 when lanes l and l + 32 carry the same env).
