@@ -210,8 +210,9 @@ def _run_rank(args, rank, world, local_rank):
             "config2_hover_4096_one_launch": _kstep_rate(4096, 1000, dev, args.seed),
             "hover_65536_one_launch_random": _kstep_rate(65536, 200, dev, args.seed),
             "config5_traj_ctbr_65536": _kernel_rate(65536, "trajectory", "RateControlWrapper", dev, args.seed),
-            "hover_ctbr_65536": _kernel_rate(65536, "hover", "RateControlWrapper", dev, args.seed),
-            "config1_train_py_on_gpu": _train_py_scale(dev, args.seed)}
+            "hover_ctbr_65536": _kernel_rate(65536, "hover", "RateControlWrapper", dev, args.seed)}
+        if world == 1:  # a one-process PPO (at world > 1 its construction would join the ranks' collectives)
+            res["configs"]["config1_train_py_on_gpu"] = _train_py_scale(dev, args.seed)
     del actions, g
     env.close()
     if rank == 0:

@@ -22,8 +22,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# (the rank-0-only configs run too: nothing rank 0 does alone may join a collective)
 SMALL = ["--steps", "20", "--warmup", "5", "--graph-chunk", "10", "--kernel-launches", "20",
-         "--large-envs", "0", "--dram-envs", "0", "--rollout-steps", "0", "--no-configs",
+         "--large-envs", "0", "--dram-envs", "0", "--rollout-steps", "0",
          "--no-cpu-baseline", "--e2e-iters", "1", "--e2e-steps", "16", "--e2e-epochs", "1"]
 
 
@@ -68,6 +69,7 @@ def test_two_rank_bench_line_is_verifiable():
         assert 0.0 < epr[k]["min"] <= epr[k]["max"], k
     assert all(r["allreduce_median_us"] > 0.0 for r in epr["ranks"])
     assert "per_rank" not in one and "per_rank" not in e1
+    assert "config1_train_py_on_gpu" in one["configs"] and "config1_train_py_on_gpu" not in two["configs"]
     # (b) each rank's shard is the same bits as those global ids in one handle
     si = e2["shard_identity"]
     assert si["all_equal"] and len(si["rank_digests"]) == 2 and si["one_handle_envs"] == 2 * n
