@@ -374,6 +374,38 @@ def test_graph_replayed_update_is_bit_identical(normalize):
     assert sa == sb and sa[0]["n"] == 3 * 16
 
 
+def test_graph_update_recaptures_on_resumed_state_and_new_lr():
+    """The captured epoch graph holds the Adam state tensors' pointers and the learning rate as
+    kernel arguments. After PPO.load_state_dict (which replaces the optimizer's state tensors) and a
+    changed lr, the graph path must recapture and stay bit-identical to the eager loop: iteration 1,
+    snapshot, iteration 2, load the snapshot, lr x 2, iteration 3."""
+    import copy
+    from uav_reinforcement_learning_control_amd.envs import QuadVecEnv
+    from uav_reinforcement_learning_control_amd.ppo.ppo import PPO, PPOConfig
+    outs = []
+    for graph in (True, False):
+        env = QuadVecEnv(8, env="hover", wrapper="RateControlWrapper", device="cuda:0", seed=3)
+        cfg = PPOConfig(n_steps=256, batch_size=128, n_epochs=2, graph_update=graph)
+        algo = PPO(env, cfg, seed=11)
+        torch.manual_seed(5)
+        algo.collect_rollouts()
+        algo.train()
+        snap = copy.deepcopy(algo.state_dict())
+        algo.collect_rollouts()
+        algo.train()
+        algo.load_state_dict(snap)
+        algo.opt.param_groups[0]["lr"] *= 2.0
+        algo.collect_rollouts()
+        algo.train()
+        assert (algo._epoch_graph is not None) == graph
+        st = algo.opt.state
+        outs.append([p.detach().clone() for p in algo.policy.parameters()] +
+                    [st[p][k].clone() for p in algo.policy.parameters() for k in ("exp_avg", "exp_avg_sq", "step")])
+        env.close()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("max_norm", [0.5, 1e9, 0.0])
 def test_fused_clip_adam_matches_torch(max_norm):
     """quad_clip_adam (clip_grad_norm_ + Adam.step) vs torch's on identical gradients, 4 steps, on

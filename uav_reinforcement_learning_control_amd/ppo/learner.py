@@ -194,6 +194,15 @@ class FusedAdam:
         a.lr, a.beta1, a.beta2, a.eps, a.max_grad_norm = float(grp["lr"]), b1, b2, float(grp["eps"]), self.max_grad_norm
         return a
 
+    def signature(self) -> tuple:
+        """Everything a quad_clip_adam launch takes by value: the parameter, gradient and Adam-state
+        pointers and the hyperparameters. A hipGraph that captured step() replays correctly only
+        while this is unchanged (Optimizer.load_state_dict replaces the state tensors; a changed
+        lr is a new kernel argument)."""
+        a = self._build()
+        return tuple((a.params[i], a.grads[i], a.exp_avg[i], a.exp_avg_sq[i], a.step[i]) for i in range(a.count)) + \
+            (a.lr, a.beta1, a.beta2, a.eps, a.max_grad_norm)
+
     def step(self) -> None:
         a = self._build()
         if self._ws is None:

@@ -514,9 +514,12 @@ class PPO:
         permutation is drawn into its buffer -- the same kernels on the same data in the same
         order as the eager loop (the same bits), without its per-launch host work (at train.py's
         scale, 8 envs x 1,024 steps in minibatches of 128, that host work was most of the update).
-        The first epoch after a (re)capture runs eagerly; its launches warm the workspaces."""
+        The first epoch after a (re)capture runs eagerly; its launches warm the workspaces. The graph
+        is recaptured whenever anything its launches took by value changes: the buffers, the batch
+        partition, or the optimizer's state tensors / hyperparameters (FusedAdam.signature)."""
         total, dev = obs.shape[0], self.device
-        key = (B, nmb, obs.data_ptr(), adv.data_ptr(), self._learner.normalize_advantage)
+        key = (B, nmb, tuple(t.data_ptr() for t in (obs, act, logp_old, adv, ret)),
+               self._learner.normalize_advantage, self._adam.signature())
         mstats = torch.zeros(epochs * nmb, 4, dtype=torch.float32, device=dev)
         e0 = 0
         if self._epoch_graph is None or self._epoch_graph[0] != key:
@@ -569,6 +572,7 @@ class PPO:
         for st in self.opt.state.values():  # fused Adam keeps its step counters on the device
             if "step" in st and torch.is_tensor(st["step"]):
                 st["step"] = st["step"].to(device=self.device, dtype=torch.float32)
+        self._epoch_graph = None  # its launches hold the replaced Adam state tensors
         self.num_timesteps = int(sd["num_timesteps"])
         ns = int(sd.get("noise_step", 0))
         self._t_host = ns
