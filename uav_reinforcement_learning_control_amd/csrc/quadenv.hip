@@ -238,10 +238,22 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
 #pragma unroll
       for (int j = 0; j < 4; j++) u16[4 * b + j] = u01(cw[j]);
     }
+#if defined(QD_ABL_HDRAW0)  // cost ablation (tools only): the helper's reset row without its Philox words
+#pragma unroll
+    for (int j = 0; j < 16; j++) u16[j] = u01(uint32_t(i) * 0x9E3779B9u + ep * 0x85EBCA6Bu + uint32_t(j) * 0xC2B2AE35u);
+#endif
     float init12[12], tgt[3], obs[12], s12[12];
     reset_affine_u(K.init_lo, K.init_span, K.tgt_lo, K.tgt_span, u16, init12, tgt);
     EnvRegs<float> e;
     env_reset_from<float, KIND>(K, e, init12, tgt, obs, s12);
+#if defined(QD_ABL_HROW0)  // cost ablation (tools only): no reset row at all (zeros)
+#pragma unroll
+    for (int j = 0; j < 3; j++) { e.pos[j] = e.v[j] = e.w[j] = e.target[j] = 0.f; }
+#pragma unroll
+    for (int j = 0; j < 4; j++) e.q[j] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 12; j++) obs[j] = 0.f;
+#endif
     const float row[HROW] = {e.pos[0], e.pos[1], e.pos[2], e.q[0], e.q[1], e.q[2], e.q[3],
                              e.v[0], e.v[1], e.v[2], e.w[0], e.w[1], e.w[2],
                              e.target[0], e.target[1], e.target[2],
@@ -273,7 +285,9 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
     float qn[4] = {e.q[0], e.q[1], e.q[2], e.q[3]};
     normalize4(qn);
     ForceAcc<float> fa;
+#if !defined(QD_ABL_NOPHYSH)  // cost ablation (tools only): k_step_h without the rigid-body step
     forward_base(K.ph, qn, e.th, e.v, e.w, e.s, fa);
+#endif
     if (stamps) { QD_PIN_N(fa.FB, 3); QD_PIN_N(fa.tau, 3); QD_PIN_N(fa.Qs, 4); QD_PIN_N(fa.R, 9); }
     QD_STAMP(stamps, 2);
     __syncthreads();  // (C)
@@ -303,7 +317,11 @@ __device__ __forceinline__ void step_h_body(const KConsts<float>& K, KParams p, 
       const double z[4] = {0.0, 0.0, 0.0, 0.0};
       m = wrench_of<float, true>(K.ph, z, true);
     }
+#if !defined(QD_ABL_NOPHYSH)
     physics_finish<float, true>(K.ph, e, qn, fa, m);
+#else
+    e.pos[0] += m.Fsum * 1e-9f;  // keeps the control hand-off live
+#endif
     if (stamps) { QD_PIN_N(e.pos, 3); QD_PIN_N(e.q, 4); QD_PIN_N(e.v, 3); QD_PIN_N(e.w, 3); }
     QD_STAMP(stamps, 4);
     StepRes r;
