@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 
 VARIANTS = [("base", "2"), ("NOENV", "2"), ("base", "2"), ("NOMLP", "2"), ("base", "2"), ("NOCRITIC", "2")]
 if os.environ.get("ROLL_VARIANTS"):  # e.g. "base,NTBUF,base,NTBUF" (tools/_build/roll_<name>.so)
-    VARIANTS = [(v, "2") for v in os.environ["ROLL_VARIANTS"].split(",")]
+    VARIANTS = [tuple((v + ":2").split(":")[:2]) for v in os.environ["ROLL_VARIANTS"].split(",")]  # name[:NT]
 
 
 def main():
