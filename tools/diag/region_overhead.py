@@ -89,7 +89,31 @@ def main():
         stream.synchronize()
         return time.perf_counter() - t0
 
-    vs = {"A_bench_region": va, "B_no_events": vb, "C_e0_outside": vc, "D_ctypes_launch": vd, "E_stream_sync": ve}
+    hip.hipEventCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
+    hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+    hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+
+    def hev(flags):
+        e = C.c_void_p()
+        assert hip.hipEventCreateWithFlags(C.byref(e), flags) == 0
+        return e
+
+    fev = {0x20000000: (hev(0x20000000), hev(0x20000000)), 0x40000000: (hev(0x40000000), hev(0x40000000))}
+
+    def vf(flags):
+        def f():
+            a, b = fev[flags]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            hip.hipEventRecord(a, sp)
+            g.replay()
+            hip.hipEventRecord(b, sp)
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0
+        return f
+
+    vs = {"A_bench_region": va, "B_no_events": vb, "C_e0_outside": vc, "D_ctypes_launch": vd, "E_stream_sync": ve,
+          "F_ev_nosysfence": vf(0x20000000), "G_ev_releasedev": vf(0x40000000)}
     res = {k: [] for k in vs}
     for _ in range(a.reps):
         for k, f in vs.items():
