@@ -75,52 +75,6 @@ def _graph_upload(g) -> None:
         pass  # older torch without raw_cuda_graph_exec: the untimed warm replay below covers it
 
 
-class _RegionEvents:
-    """The timed region's HIP event pair, created with hipEventReleaseToDevice: the markers release
-    to device scope only, which the HIP API documents for more precise timing of the commands between
-    two events (a default event's system-scope release writes back and invalidates the caches). The
-    region still ends with torch.cuda.synchronize(). Falls back to torch's events if the runtime
-    refuses the flag. Measured: ~3 us less wall per 20-launch region than torch's default events
-    (profiles/r06/region_overhead_events.txt)."""
-    FLAGS = 0x40000000  # hipEventReleaseToDevice
-
-    def __init__(self):
-        self.hip = None
-        try:
-            hip = C.CDLL("libamdhip64.so.7")
-            hip.hipEventCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
-            hip.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
-            hip.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
-            hip.hipEventDestroy.argtypes = [C.c_void_p]
-            ev = [C.c_void_p(), C.c_void_p()]
-            if all(hip.hipEventCreateWithFlags(C.byref(e), self.FLAGS) == 0 for e in ev):
-                self.hip, self.ev = hip, ev
-        except (AttributeError, OSError):
-            pass
-        if self.hip is None:
-            self.tev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-
-    def record(self, k: int) -> None:
-        if self.hip is None:
-            self.tev[k].record()
-        elif self.hip.hipEventRecord(self.ev[k], C.c_void_p(torch.cuda.current_stream().cuda_stream)) != 0:
-            raise RuntimeError("hipEventRecord failed")
-
-    def elapsed_ms(self) -> float:
-        if self.hip is None:
-            return self.tev[0].elapsed_time(self.tev[1])
-        ms = C.c_float()
-        if self.hip.hipEventElapsedTime(C.byref(ms), self.ev[0], self.ev[1]) != 0:
-            raise RuntimeError("hipEventElapsedTime failed")
-        return float(ms.value)
-
-    def close(self) -> None:
-        if self.hip is not None:
-            for e in self.ev:
-                self.hip.hipEventDestroy(e)
-            self.hip = None
-
-
 def _gated_kernel_us(step, actions, n_launch: int = 200) -> float:
     """Average device time per launch of back-to-back graph-replayed step launches, HIP events on
     the launching stream. A short spin kernel ahead of the first event keeps the GPU busy while
@@ -201,21 +155,19 @@ def _run_rank(args, rank, world, local_rank):
 
     def region(graphs):
         """barrier + synchronize, the replays between two HIP events (on the stream the kernels
-        run on: the device time of the same region), synchronize; returns (wall s, device ms)"""
-        ev = _RegionEvents()
+        run on: the device time of the same region), synchronize; returns (wall s, e0, e1)"""
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
-        ev.record(0)
+        e0.record()
         for gr in graphs:
             gr.replay()
-        ev.record(1)
+        e1.record()
         torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
-        ms = ev.elapsed_ms()
-        ev.close()
-        return wall, ms
+        return time.perf_counter() - t0, e0, e1
 
     # the timed step sequence as hipGraph(s), captured and uploaded before the warmup; the W
     # warmup steps are replays of a graph of the same launches (first kernel runs, caches, TLB),
@@ -227,12 +179,12 @@ def _run_rank(args, rank, world, local_rank):
         region([gw])
 
     # timed region: exactly K steps, barrier + synchronize on both sides
-    elapsed, region_ms = region([g] * (args.steps // chunk))
+    elapsed, e0, e1 = region([g] * (args.steps // chunk))
     # the closing barrier follows this rank's clock stop: its RCCL latency (tens of us against a
     # ~130 us 20-step region) is not step work; the MAX over ranks below is the slowest rank's K steps
     if world > 1:
         dist.barrier()
-    region_us = region_ms * 1e3 / args.steps
+    region_us = e0.elapsed_time(e1) * 1e3 / args.steps
     own_elapsed = elapsed
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
